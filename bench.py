@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark: option-prices/sec (+ calibrations/sec) of the COS calibration objective on MI355X.
+
+Workload (BASELINE.json configs[1], the single-GPU config the metric is quoted on):
+  "c2": a 1,024-option synthetic surface (32 K/S in linspace(0.8, 1.2) x 32 T in
+  linspace(0.1, 2.0), calls, S0 = 100, r = 0.03, market = model at a seed-1 parameter draw x
+  (1 + N(0, 0.02)), seed 2), COS N = 256.  One step = one L-BFGS-B function+gradient request =
+  the 14 SciPy forward-difference points (13 parameters + base) priced over all 1,024 options and
+  reduced to 14 losses: 14,336 option prices per step.  Each step uses a different x (different
+  param sets), all inputs resident in HBM before the timed region; the steps are issued back to
+  back on one stream (independent requests, as in lockstep multi-start).
+
+Multi-GPU (torchrun, one process per GPU): weak scaling -- every rank runs its own independent
+requests (multi-start sharding has no data-path collective); timing is the max over ranks;
+value = all ranks' prices / that time.
+
+Also reported: roofline of the dominant kernel (cos_price_kernel) from HIP events on its stream,
+a full single-start calibration of the same surface (calibrations/sec), and a CPU baseline (the
+scalar-structured NumPy port in oracle/, timed on a bounded sample on rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch                      # imported first: torch and libdhcos share one HIP runtime
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "option-pricing-ffn-lbfgs_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from dhcos import _native                                      # noqa: E402
+from dhcos.calibrator import (DoubleHestonJumpCalibrator,      # noqa: E402
+                              fd_request_points, x_to_model)
+
+# algorithmic work convention (DESIGN.md "Roofline"): fp64 flop-equivalents
+FLOP_CF = 716          # per unique characteristic-function evaluation (incl. e^{-iua} phase)
+FLOP_TERM = 120        # per (param set, option, COS term): payoff coefficients + accumulate
+PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector peak (spec)
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+BYTES_PER_OPTION = 8 + 8 + 1 + 8 + 4   # K, T, is_call, mkt, perm read per (param set, option)
+
+GEN_LO = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
+GEN_HI = np.array([0.08, 4.5, 0.065, 0.5, -0.4, 0.07, 1.2, 0.07, 0.35, -0.2, 0.25, -0.01, 0.12])
+
+
+def make_surface(nK, nT, seed_params=1, seed_noise=2, S0=100.0, r=0.03, N=256, put_itm=False):
+    """Synthetic market of SURVEY 8(d): model prices at a seed-1 draw, 2% noise (seed 2)."""
+    kk, tt = np.meshgrid(np.linspace(0.8, 1.2, nK) * S0, np.linspace(0.1, 2.0, nT))
+    K, T = kk.ravel(), tt.ravel()
+    call = np.ones(K.size, dtype=bool) if not put_itm else (K >= S0)
+    true = GEN_LO + (GEN_HI - GEN_LO) * np.random.RandomState(seed_params).rand(13)
+    rec = np.zeros((1, 16))
+    rec[0, :13], rec[0, 13], rec[0, 14] = true, S0, r
+    ctx = _native.default_context()
+    model = _native.Surface(ctx, K, T, call).price(rec, N)[0]
+    mkt = model * (1 + np.random.RandomState(seed_noise).normal(0, 0.02, K.size))
+    opts = [{"strike": float(k), "maturity": float(t), "price": float(p),
+             "option_type": "call" if c else "put"} for k, t, p, c in zip(K, T, mkt, call)]
+    return opts, S0, r
+
+
+def step_params(cal, n_steps, starts, seed):
+    """[n_steps, 14*starts, 16] param records: FD points around distinct x per step."""
+    rs = np.random.RandomState(seed)
+    x0 = cal.get_initial_guess(0)
+    out = np.empty((n_steps, 14 * starts, 16))
+    for i in range(n_steps):
+        X = np.concatenate([fd_request_points(x0 + rs.normal(0, 0.05, 13))[0] for _ in range(starts)])
+        out[i, :, :13] = x_to_model(X)
+        out[i, :, 13], out[i, :, 14], out[i, :, 15] = cal.spot, cal.risk_free_rate, 0.0
+    return out
+
+
+def cpu_baseline(cal_opts, S0, r, N, budget_s=12.0):
+    """Scalar-structured NumPy port (oracle/) of the reference pricer, 1 core, bounded sample."""
+    from oracle import dh_oracle as O
+    x = DoubleHestonJumpCalibrator(S0, r, cal_opts).get_initial_guess(0)
+    prm = O.to_params(x)
+    n, t0 = 0, time.perf_counter()
+    with np.errstate(all="ignore"):
+        while True:
+            o = cal_opts[(n * 37) % len(cal_opts)]
+            O.price_scalar(prm, S0, o["strike"], o["maturity"], r, o["option_type"] == "call", N)
+            n += 1
+            if time.perf_counter() - t0 > budget_s and n >= 16:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "option-prices/s", "cores": 1, "kind": "port",
+            "sample": f"{n} options of the workload surface priced one by one at N={N} by "
+                      f"oracle.dh_oracle.price_scalar (reference algorithm restated) in {dt:.1f} s"}
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            return json.load(fh).get(config, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+CONFIGS = {
+    "c2": dict(nK=32, nT=32, N=256, starts=1, put_itm=False,
+               workload="1,024-option synthetic surface (32 K/S x 32 T), N=256, one L-BFGS-B "
+                        "function+gradient request (14 param sets) per step"),
+    "c3": dict(nK=100, nT=100, N=512, starts=3, put_itm=True,
+               workload="10,000-option surface (100 K/S x 100 T, puts K<S), N=512, 3 lockstep "
+                        "starts x 14 param sets per step"),
+    "c1": dict(nK=5, nT=3, N=128, starts=1, put_itm=False,
+               workload="15-option grid (5 K x 3 T), N=128, one function+gradient request"),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-calib", action="store_true", help="skip the full-calibration leg")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    os.environ["DHCOS_DEVICE"] = str(local)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    opts, S0, r = make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
+    M = len(opts)
+    cal = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"])
+    surf = cal._get_surface()
+    S = 14 * cfg["starts"]
+    K_, W_ = args.steps, args.warmup
+    host = step_params(cal, K_ + W_, cfg["starts"], seed=100 + rank)
+    d_params = torch.from_numpy(host).to(dev)
+    d_sse = torch.empty((K_ + W_, S), dtype=torch.float64, device=dev)
+    d_bad = torch.empty((K_ + W_, S), dtype=torch.int32, device=dev)
+    N = cfg["N"]
+
+    def run(i):
+        surf.loss_dev(d_params[i].data_ptr(), S, d_sse[i].data_ptr(), d_bad[i].data_ptr(), N=N,
+                      stream=sptr)
+
+    for i in range(W_):
+        run(K_ + i)
+    # correctness spot check of one step against the host API (same kernel, host copies)
+    sse_h, bad_h, _ = surf.loss_terms(host[K_], N)
+    torch.cuda.synchronize()
+    assert np.array_equal(sse_h, d_sse[K_].cpu().numpy()), "device/host path mismatch"
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K_):
+        run(i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    prices_per_step = S * M
+    value = prices_per_step * K_ * world / dt
+
+    # ---- roofline of the dominant kernel (cos_price_kernel, loss mode), HIP events ----
+    n_tiles = surf.n_tiles
+    part_sse = torch.empty(S * n_tiles, dtype=torch.float64, device=dev)
+    part_bad = torch.empty(S * n_tiles, dtype=torch.int32, device=dev)
+    reps = max(20, min(K_, 200))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for j, (e0, e1) in enumerate(evs):
+        e0.record(stream)
+        surf.partials_dev(d_params[j % K_].data_ptr(), S, part_sse.data_ptr(), part_bad.data_ptr(),
+                          N=N, stream=sptr)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    ker_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    groups = len({o["maturity"] for o in opts})
+    flop = S * groups * N * FLOP_CF + S * M * N * FLOP_TERM
+    achieved = flop / (ker_ms * 1e-3) / 1e12
+    alg_bytes = S * 16 * 8 + S * M * BYTES_PER_OPTION + S * n_tiles * 12
+    roofline = {"bound": "valu_fp64", "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4),
+                "traffic": pmc_traffic(args.config),
+                "kernel": "cos_price_kernel<256>", "kernel_ms": round(ker_ms, 5),
+                "flop_per_launch": flop, "alg_bytes_per_launch": alg_bytes,
+                "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
+                        "peak_GBs": PEAK_HBM_GBS,
+                        "frac": alg_bytes / (ker_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}}
+
+    # ---- calibrations/sec: one full single-start calibration of the same surface per rank ----
+    calib = None
+    if not args.no_calib:
+        c2 = DoubleHestonJumpCalibrator(S0, r, opts, N=N)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        res = c2.calibrate(maxiter=300, multi_start=1)
+        tc = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([tc], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            tc = float(tt.item())
+        calib = {"calibrations_per_sec": world / tc, "seconds": tc, "iterations": int(res.iterations),
+                 "final_loss": float(res.final_loss), "message": res.message,
+                 "fd_requests": int(c2.n_calls // 14)}
+
+    if rank == 0:
+        line = {
+            "metric": "option-prices/sec (COS, calibration objective) + calibrations/sec",
+            "value": value, "unit": "option-prices/s", "n_gpus": world, "steps": K_,
+            "warmup": W_, "ms_per_step": dt / K_ * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": cfg["workload"], "options": M, "cos_terms": N,
+                       "param_sets_per_step": S, "prices_per_step": prices_per_step,
+                       "parallelism": f"independent requests per rank x{world}"},
+            "roofline": roofline,
+        }
+        if calib:
+            line["calibration"] = calib
+        if not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(opts, S0, r, N, args.cpu_budget)
+            line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

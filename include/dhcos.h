@@ -1,0 +1,128 @@
+/*
+ * dhcos.h -- C-ABI of the MI355X-native Double-Heston + Merton-jump COS pricer and calibration
+ * objective (libdhcos.so, gfx950).
+ *
+ * The reference (zenthepen/Option-Pricing-FFN-LBFGS) is pure Python; it has no FFI of its own.
+ * Each entry point below replaces one reference call site on the hot path, named per function
+ * (file:line in the reference).  The Python host layer (option-pricing-ffn-lbfgs_amd/dhcos) binds
+ * these through ctypes; INTEGRATION.md shows the binding a maintainer adds on the reference side.
+ *
+ * Conventions
+ *   - Every function returns 0 on success and a negative DH_E* code on failure; the message of
+ *     the last failure on the calling thread is returned by dh_last_error().
+ *   - Numeric failures (NaN / inf / non-positive prices) are NOT errors: they are reported in the
+ *     outputs exactly as the reference produces them (see dh_surface_loss).
+ *   - "host" entry points take host pointers, copy synchronously and return when results are on
+ *     the host (the caller may free its buffers on return).  "_dev" entry points take device
+ *     pointers and enqueue on the given HIP stream (NULL = the context's own stream) without
+ *     synchronising.
+ *   - Param-set record: DH_PARAM_STRIDE (16) doubles per set:
+ *       [0..12] v01 kappa1 theta1 sigma1 rho1 v02 kappa2 theta2 sigma2 rho2 lambda_j mu_j sigma_j
+ *       [13] S0   [14] r   [15] q
+ *     (double_heston.py:26-46 constructor arguments, same meaning).
+ *   - All arithmetic is IEEE fp64.
+ */
+#ifndef DHCOS_H
+#define DHCOS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DH_PARAM_STRIDE 16
+#define DH_MAX_N 2048            /* largest COS series length accepted (LDS-resident table) */
+
+enum {
+    DH_OK = 0,
+    DH_E_ARG = -1,               /* invalid argument (null pointer, bad size, N out of range) */
+    DH_E_HIP = -2,               /* HIP runtime error (message has the HIP error string) */
+    DH_E_NODEV = -3,             /* no usable gfx950 device */
+    DH_E_ALLOC = -4              /* host/device allocation failure */
+};
+
+/* strike_mode for surfaces */
+enum {
+    DH_STRIKE_ABSOLUTE = 0,      /* K[m] is the strike */
+    DH_STRIKE_PCT_SPOT = 1       /* K[m] is K_relative; strike = K_relative * S0 / 100.0 per param
+                                    set (synthetic_generator.py:125) */
+};
+
+typedef struct dh_ctx dh_ctx;
+typedef struct dh_surface dh_surface;
+
+/* ---- context ------------------------------------------------------------------------------ */
+int dh_version(void);
+const char* dh_last_error(void);
+int dh_device_count(int* count);
+/* One context per (device, host thread).  Owns a HIP stream and grow-only device scratch. */
+int dh_ctx_create(int device, dh_ctx** out);
+int dh_ctx_destroy(dh_ctx* ctx);
+int dh_ctx_synchronize(dh_ctx* ctx);
+/* The HIP stream the context launches on (hipStream_t as void*). */
+void* dh_ctx_stream(dh_ctx* ctx);
+
+/* ---- option surfaces ---------------------------------------------------------------------- */
+/* Upload an option set once.  Options are grouped by exact maturity on the host; groups are cut
+ * into tiles of at most 256 options; every tile shares one COS/CF table per param set.
+ *   K, T, is_call: [M]   (is_call resolved by the caller as option_type.upper()[0]=='C',
+ *                         double_heston.py:172)
+ *   mkt:           [M] market prices, may be NULL (needed only by dh_surface_loss*)
+ * Replaces the per-option DoubleHeston construction in lbfgs_calibrator.py:128-150 and
+ * synthetic_generator.py:123-138.                                                           */
+int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_t* is_call,
+                      const double* mkt, int M, int strike_mode, dh_surface** out);
+int dh_surface_destroy(dh_surface* s);
+int dh_surface_size(const dh_surface* s, int* M, int* n_tiles);
+
+/* Price every option of the surface under every param set: out[p*M + m], m in the caller's
+ * original option order.  Replaces DoubleHeston.pricing(N) (double_heston.py:160-192) called
+ * P*M times.  L is the truncation width (truncationRange(L=10), double_heston.py:100).        */
+int dh_surface_price(dh_ctx* ctx, const dh_surface* s, const double* params, int64_t P, int N,
+                     double L, double* out);
+
+/* Calibration objective over the surface for S param sets (one FD request = 14 sets):
+ *   sse[s]   = sum_m ((price_sm - mkt_m) / mkt_m)^2      (lbfgs_calibrator.py:163, un-normalised)
+ *   n_bad[s] = #{m : price_sm is NaN, +-inf or <= 0}      (lbfgs_calibrator.py:152)
+ *   prices   = optional [S][M] output (NULL to skip)
+ * The host forms loss = n_bad ? 1e10 : sse / M + feller (lbfgs_calibrator.py:118-177).       */
+int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int S, int N,
+                    double L, double* sse, int32_t* n_bad, double* prices);
+
+/* Device-pointer variants: params/out/sse/n_bad are device pointers; enqueue on `stream`
+ * (hipStream_t; NULL = context stream).  No synchronisation, no allocation after warm-up.     */
+int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int64_t P,
+                         int N, double L, double* d_out, void* stream);
+int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S, int N,
+                        double L, double* d_sse, int32_t* d_n_bad, double* d_prices,
+                        void* stream);
+
+/* First stage of dh_surface_loss_dev only (the COS kernel in loss mode): writes one
+ * (sse, n_bad) partial per (param set, tile) into d_part_sse / d_part_bad [S * n_tiles].
+ * Exposed so a caller (bench.py) can time the dominant kernel alone.                         */
+int dh_surface_partials_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S,
+                            int N, double L, double* d_part_sse, int32_t* d_part_bad,
+                            void* stream);
+
+/* ---- paired pricing: option i under param set i ------------------------------------------- */
+/* out[i] = price of (K[i], T[i], is_call[i]) under params[i]; replaces a loop of single
+ * DoubleHeston(...).pricing(N) calls (double_heston.py:160-192).                              */
+int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const double* T,
+                   const int8_t* is_call, int64_t P, int N, double L, double* out);
+
+/* ---- building blocks (exposed for API parity with the reference's public methods) -------- */
+/* phi(u_j; tau) for one param set: DoubleHeston.characteristic_function (double_heston.py:48-97) */
+int dh_cf(dh_ctx* ctx, const double* params, const double* u, int n, double tau, double* re,
+          double* im);
+/* [a_i, b_i] for param set i and option i: DoubleHeston.truncationRange (double_heston.py:100-139) */
+int dh_trunc_range(dh_ctx* ctx, const double* params, const double* K, const double* T,
+                   int64_t P, double L, double* a, double* b);
+/* chi_k / psi_k for integer k_j on [c,d] within [a,b]: double_heston.py:141-158 */
+int dh_cos_coeffs(dh_ctx* ctx, const int32_t* k, int n, double c, double d, double a, double b,
+                  double* chi, double* psi);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DHCOS_H */

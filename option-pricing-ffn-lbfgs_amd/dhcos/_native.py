@@ -1,0 +1,285 @@
+"""ctypes binding of libdhcos.so (the gfx950 C-ABI declared in include/dhcos.h).
+
+The library is loaded lazily on first use from this package directory (built in-tree by
+``make -C option-pricing-ffn-lbfgs_amd/csrc`` or ``__graft_entry__.build()``).  There is no CPU
+fallback: if the library or a gfx950 device is missing, every compute entry point raises
+``NativeError``.
+
+HIP runtime sharing: torch-ROCm ships its own libamdhip64.so.  If a process uses both torch (e.g.
+bench.py, torch.distributed) and this library, torch must be imported *before* the first call here
+so that both bind to one HIP runtime; ``runtime_shared_with_torch()`` checks it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DHCOS_LIB", os.path.join(_HERE, "libdhcos.so"))
+
+PARAM_STRIDE = 16
+MAX_N = 2048
+STRIKE_ABSOLUTE = 0
+STRIKE_PCT_SPOT = 1
+
+_dp = C.POINTER(C.c_double)
+_i8p = C.POINTER(C.c_int8)
+_i32p = C.POINTER(C.c_int32)
+_vp = C.c_void_p
+
+# name -> (restype, argtypes); mirrors include/dhcos.h one to one
+SIGNATURES = {
+    "dh_version": (C.c_int, []),
+    "dh_last_error": (C.c_char_p, []),
+    "dh_device_count": (C.c_int, [_i32p]),
+    "dh_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "dh_ctx_destroy": (C.c_int, [_vp]),
+    "dh_ctx_synchronize": (C.c_int, [_vp]),
+    "dh_ctx_stream": (_vp, [_vp]),
+    "dh_surface_create": (C.c_int, [_vp, _dp, _dp, _i8p, _dp, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "dh_surface_destroy": (C.c_int, [_vp]),
+    "dh_surface_size": (C.c_int, [_vp, _i32p, _i32p]),
+    "dh_surface_price": (C.c_int, [_vp, _vp, _dp, C.c_int64, C.c_int, C.c_double, _dp]),
+    "dh_surface_loss": (C.c_int, [_vp, _vp, _dp, C.c_int, C.c_int, C.c_double, _dp, _i32p, _dp]),
+    "dh_surface_price_dev": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp, _vp]),
+    "dh_surface_loss_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp,
+                                      _vp]),
+    "dh_surface_partials_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp,
+                                          _vp]),
+    "dh_price_pairs": (C.c_int, [_vp, _dp, _dp, _dp, _i8p, C.c_int64, C.c_int, C.c_double, _dp]),
+    "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
+    "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
+    "dh_cos_coeffs": (C.c_int, [_vp, _i32p, C.c_int, C.c_double, C.c_double, C.c_double,
+                                C.c_double, _dp, _dp]),
+}
+
+
+class NativeError(RuntimeError):
+    """Raised for any failure of the native (HIP) path; there is no fallback."""
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load():
+    """Load libdhcos.so (once) and attach the C signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeError(
+                    f"libdhcos.so not found at {LIB_PATH}; build it with "
+                    "`make -C option-pricing-ffn-lbfgs_amd/csrc` (hipcc, gfx950)")
+            lib = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        msg = load().dh_last_error()
+        raise NativeError(f"libdhcos error {rc}: {msg.decode() if msg else ''}")
+
+
+def runtime_shared_with_torch() -> bool:
+    """True unless two different libamdhip64 images are mapped into this process."""
+    try:
+        with open("/proc/self/maps") as fh:
+            paths = {ln.split()[-1] for ln in fh if "libamdhip64" in ln}
+    except OSError:
+        return True
+    return len({os.path.realpath(p) for p in paths}) <= 1
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    rc = load().dh_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _ptr(a, ty=_dp):
+    return a.ctypes.data_as(ty)
+
+
+class Context:
+    """A device context: one HIP stream + grow-only device scratch (dh_ctx)."""
+
+    def __init__(self, device: int = 0):
+        lib = load()
+        h = _vp()
+        _check(lib.dh_ctx_create(int(device), C.byref(h)))
+        self._h = h
+        self.device = int(device)
+        self._lock = threading.Lock()
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return load().dh_ctx_stream(self._h) or 0
+
+    def synchronize(self):
+        _check(load().dh_ctx_synchronize(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().dh_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- pricing primitives -------------------------------------------------------------
+    def price_pairs(self, params, K, T, is_call, N=128, L=10.0):
+        params = _f64(params).reshape(-1, PARAM_STRIDE)
+        P = params.shape[0]
+        K, T = _f64(K).reshape(P), _f64(T).reshape(P)
+        ic = np.ascontiguousarray(is_call, dtype=np.int8).reshape(P)
+        out = np.empty(P)
+        with self._lock:
+            _check(load().dh_price_pairs(self._h, _ptr(params), _ptr(K), _ptr(T), _ptr(ic, _i8p),
+                                         P, int(N), float(L), _ptr(out)))
+        return out
+
+    def cf(self, params16, u, tau):
+        p = _f64(params16).reshape(PARAM_STRIDE)
+        u = _f64(u).reshape(-1)
+        re, im = np.empty(u.size), np.empty(u.size)
+        with self._lock:
+            _check(load().dh_cf(self._h, _ptr(p), _ptr(u), u.size, float(tau), _ptr(re), _ptr(im)))
+        return re + 1j * im
+
+    def trunc_range(self, params, K, T, L=10.0):
+        params = _f64(params).reshape(-1, PARAM_STRIDE)
+        P = params.shape[0]
+        K, T = _f64(K).reshape(P), _f64(T).reshape(P)
+        a, b = np.empty(P), np.empty(P)
+        with self._lock:
+            _check(load().dh_trunc_range(self._h, _ptr(params), _ptr(K), _ptr(T), P, float(L),
+                                         _ptr(a), _ptr(b)))
+        return a, b
+
+    def cos_coeffs(self, k, c, d, a, b):
+        k = np.ascontiguousarray(k, dtype=np.int32).reshape(-1)
+        chi, psi = np.empty(k.size), np.empty(k.size)
+        with self._lock:
+            _check(load().dh_cos_coeffs(self._h, _ptr(k, _i32p), k.size, float(c), float(d),
+                                        float(a), float(b), _ptr(chi), _ptr(psi)))
+        return chi, psi
+
+
+class Surface:
+    """An option set resident in HBM, grouped by maturity into <=256-option tiles (dh_surface)."""
+
+    def __init__(self, ctx: Context, K, T, is_call, mkt=None, strike_mode=STRIKE_ABSOLUTE):
+        self.ctx = ctx
+        K, T = _f64(K).reshape(-1), _f64(T).reshape(-1)
+        M = K.size
+        if T.size != M:
+            raise ValueError("K and T differ in length")
+        ic = np.ascontiguousarray(is_call, dtype=np.int8).reshape(M)
+        mk = None if mkt is None else _f64(mkt).reshape(M)
+        h = _vp()
+        _check(load().dh_surface_create(ctx.handle, _ptr(K), _ptr(T), _ptr(ic, _i8p),
+                                        None if mk is None else _ptr(mk), M, int(strike_mode),
+                                        C.byref(h)))
+        self._h = h
+        self.M = M
+        m, nt = C.c_int32(0), C.c_int32(0)
+        _check(load().dh_surface_size(h, C.byref(m), C.byref(nt)))
+        self.n_tiles = nt.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().dh_surface_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def price(self, params, N=128, L=10.0):
+        params = _f64(params).reshape(-1, PARAM_STRIDE)
+        P = params.shape[0]
+        out = np.empty((P, self.M))
+        with self.ctx._lock:
+            _check(load().dh_surface_price(self.ctx.handle, self._h, _ptr(params), P, int(N),
+                                           float(L), _ptr(out)))
+        return out
+
+    def loss_terms(self, params, N=128, L=10.0, want_prices=False):
+        """-> (sse[S], n_bad[S], prices[S,M] or None)."""
+        params = _f64(params).reshape(-1, PARAM_STRIDE)
+        S = params.shape[0]
+        sse = np.empty(S)
+        bad = np.empty(S, dtype=np.int32)
+        prices = np.empty((S, self.M)) if want_prices else None
+        with self.ctx._lock:
+            _check(load().dh_surface_loss(self.ctx.handle, self._h, _ptr(params), S, int(N),
+                                          float(L), _ptr(sse), _ptr(bad, _i32p),
+                                          None if prices is None else _ptr(prices)))
+        return sse, bad, prices
+
+    # device-pointer variants (torch tensors or raw device addresses)
+    def price_dev(self, d_params: int, P: int, d_out: int, N=128, L=10.0, stream: int = 0):
+        _check(load().dh_surface_price_dev(self.ctx.handle, self._h, _vp(d_params), int(P), int(N),
+                                           float(L), _vp(d_out), _vp(stream) if stream else None))
+
+    def loss_dev(self, d_params: int, S: int, d_sse: int, d_bad: int, d_prices: int = 0, N=128,
+                 L=10.0, stream: int = 0):
+        _check(load().dh_surface_loss_dev(self.ctx.handle, self._h, _vp(d_params), int(S), int(N),
+                                          float(L), _vp(d_sse), _vp(d_bad),
+                                          _vp(d_prices) if d_prices else None,
+                                          _vp(stream) if stream else None))
+
+    def partials_dev(self, d_params: int, S: int, d_part_sse: int, d_part_bad: int, N=128,
+                     L=10.0, stream: int = 0):
+        _check(load().dh_surface_partials_dev(self.ctx.handle, self._h, _vp(d_params), int(S),
+                                              int(N), float(L), _vp(d_part_sse), _vp(d_part_bad),
+                                              _vp(stream) if stream else None))
+
+
+_tls = threading.local()
+
+
+def default_context(device: int | None = None) -> Context:
+    """Per-thread cached context on ``device`` (default: $DHCOS_DEVICE or 0)."""
+    if device is None:
+        device = int(os.environ.get("DHCOS_DEVICE", "0"))
+    cache = getattr(_tls, "ctxs", None)
+    if cache is None:
+        cache = _tls.ctxs = {}
+    ctx = cache.get(device)
+    if ctx is None:
+        ctx = cache[device] = Context(device)
+    return ctx
+
+
+__all__ = ["Context", "Surface", "NativeError", "load", "default_context", "device_count",
+           "runtime_shared_with_torch", "PARAM_STRIDE", "MAX_N", "STRIKE_ABSOLUTE",
+           "STRIKE_PCT_SPOT", "LIB_PATH", "SIGNATURES"]

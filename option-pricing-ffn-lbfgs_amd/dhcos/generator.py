@@ -1,0 +1,148 @@
+"""Batch path of the synthetic calibration-data generator on the gfx950 pricer.
+
+Reference: src/data/synthetic_generator.py:25-234.  Per sample the reference draws 13 uniforms,
+blends them AR(1) (alpha = 0.9) into the previous sample, random-walks the spot, prices a 5 x 3
+call grid one option at a time and adds 2% Gaussian noise to each price.  Pricing consumes no
+randomness, so this implementation
+
+  1. draws every random number on the host in the reference's order from the legacy global
+     ``np.random`` stream (13 uniforms, then one spot normal for i > 0, then 15 noise normals:
+     vectorised per sample, same values as the reference's scalar calls),
+  2. runs the AR(1) and spot recursions on the host,
+  3. prices all samples x options in one launch per chunk on the GPU (strikes formed on the device
+     as K_relative * spot / 100.0, exactly the reference's expression, :125),
+  4. applies the noise and the per-sample loss with the reference's NumPy expressions.
+
+Output: ``list[CalibrationResult]`` pickled to ``save_path`` (as the reference), or, with
+``as_arrays=True``, a dict of columnar arrays (no per-sample Python objects, for 10^6 samples).
+"""
+from __future__ import annotations
+
+import pickle
+from datetime import datetime, timedelta
+
+import numpy as np
+
+from . import _native
+from .calibrator import CalibrationResult
+
+# synthetic_generator.py:75-89, in the reference's dict order
+PARAM_RANGES = {
+    "v1_0": (0.025, 0.080), "kappa1": (1.5, 4.5), "theta1": (0.025, 0.065),
+    "sigma1": (0.20, 0.50), "rho1": (-0.85, -0.40), "v2_0": (0.020, 0.070),
+    "kappa2": (0.30, 1.20), "theta2": (0.025, 0.070), "sigma2": (0.10, 0.35),
+    "rho2": (-0.70, -0.20), "lambda_j": (0.05, 0.25), "mu_j": (-0.08, -0.01),
+    "sigma_j": (0.03, 0.12),
+}
+STRIKES_PCT = np.array([90, 95, 100, 105, 110])   # :91
+MATURITIES = np.array([0.25, 0.5, 1.0])           # :92
+SPOT_BASE = 100.0                                  # :93
+RISK_FREE = 0.03                                   # :94
+ALPHA = 0.9                                        # :108
+
+
+def trading_dates(n):
+    """Weekdays from 2022-01-03 (synthetic_generator.py:59-67)."""
+    out, cur = [], datetime(2022, 1, 3)
+    for _ in range(n):
+        while cur.weekday() >= 5:
+            cur += timedelta(days=1)
+        out.append(cur.strftime("%Y-%m-%d"))
+        cur += timedelta(days=1)
+    return out
+
+
+def draw_paths(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
+    """Host part: RNG in reference order + AR(1) params + spot walk.
+    Returns (params [n,13], spots [n], noise [n, n_opts])."""
+    lo = np.array([v[0] for v in PARAM_RANGES.values()])
+    hi = np.array([v[1] for v in PARAM_RANGES.values()])
+    n_opt = len(strikes) * len(maturities)
+    params = np.empty((n_samples, 13))
+    spots = np.empty(n_samples)
+    noise = np.empty((n_samples, n_opt))
+    prev, spot = None, SPOT_BASE
+    for i in range(n_samples):
+        draw = np.random.uniform(lo, hi)                       # 13 draws, dict order (:101-102)
+        if prev is not None:
+            cur = ALPHA * prev + (1 - ALPHA) * draw            # (:105-109)
+        else:
+            cur = draw
+        if i > 0:
+            spot = spot * (1 + np.random.normal(0.0003, 0.01))  # (:112-116)
+        noise[i] = np.random.normal(0, 0.02, n_opt)           # one per option, grid order (:141)
+        params[i], spots[i], prev = cur, spot, cur
+    return params, spots, noise
+
+
+def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES, r=RISK_FREE,
+               chunk=1 << 18, device=None):
+    """GPU: price every sample's call grid (T outer, K inner -- the reference's loop order)."""
+    ctx = _native.default_context(device)
+    Krel = np.tile(np.asarray(strikes, dtype=np.float64), len(maturities))
+    T = np.repeat(np.asarray(maturities, dtype=np.float64), len(strikes))
+    surf = _native.Surface(ctx, Krel, T, np.ones(T.size, dtype=np.int8),
+                           strike_mode=_native.STRIKE_PCT_SPOT)
+    n = params.shape[0]
+    out = np.empty((n, T.size))
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        rec = np.empty((e - s, _native.PARAM_STRIDE))
+        rec[:, :13] = params[s:e]
+        rec[:, 13] = spots[s:e]
+        rec[:, 14] = r
+        rec[:, 15] = 0.0
+        out[s:e] = surf.price(rec, N)
+    surf.close()
+    return out
+
+
+def generate_synthetic_calibrations(n_samples: int = 500,
+                                    save_path: str = "lbfgs_calibrations_synthetic.pkl", *,
+                                    N: int = 128, device=None, as_arrays: bool = False,
+                                    verbose: bool = True):
+    """Generate ``n_samples`` synthetic calibrations (synthetic_generator.py:25-234)."""
+    say = print if verbose else (lambda *a, **k: None)
+    say("=" * 70)
+    say("GENERATING SYNTHETIC HISTORICAL CALIBRATIONS (MI355X batch path)")
+    say("=" * 70)
+    say(f"  samples: {n_samples}   save path: {save_path}   COS terms: {N}")
+    dates = trading_dates(n_samples)
+    params, spots, noise = draw_paths(n_samples)
+    model = price_grid(params, spots, N=N, device=device)
+    market = model + noise * model                                   # (:141-142)
+    rel = (model - market) / market
+    losses = np.mean(rel ** 2, axis=1)                               # (:154-157)
+    names = list(PARAM_RANGES.keys())
+    Krel = np.tile(STRIKES_PCT, len(MATURITIES))
+    Tg = np.repeat(MATURITIES, len(STRIKES_PCT))
+    if as_arrays:
+        result = dict(dates=np.array(dates), spot=spots, risk_free=RISK_FREE, params=params,
+                      param_names=names, market_prices=market, model_prices=model,
+                      strikes=(Krel[None, :] * spots[:, None]) / 100.0,
+                      maturities=Tg, final_loss=losses)
+        if save_path:
+            np.savez(save_path if save_path.endswith(".npz") else save_path + ".npz",
+                     **{k: v for k, v in result.items() if k != "param_names"},
+                     param_names=np.array(names))
+        return result
+    calibrations = []
+    for i in range(n_samples):
+        opts = [{"strike": Krel[j] * spots[i] / 100.0, "maturity": Tg[j],
+                 "price": market[i, j], "option_type": "call"} for j in range(Tg.size)]
+        calibrations.append(CalibrationResult(
+            date=dates[i], spot=spots[i], risk_free=RISK_FREE,
+            parameters={nm: params[i, k] for k, nm in enumerate(names)},
+            market_prices=market[i], model_prices=model[i], market_options=opts,
+            final_loss=losses[i], calibration_time=None, success=True, iterations=None,
+            message="Synthetic data (not from real calibration)"))
+        if verbose and (i + 1) % 50 == 0 and n_samples <= 10000:
+            say(f"  Progress: {i + 1}/{n_samples} ({(i + 1) / n_samples * 100:.1f}%)")
+    if save_path:
+        with open(save_path, "wb") as fh:
+            pickle.dump(calibrations, fh)
+    if verbose and n_samples:
+        errs = np.abs((model - market) / market) * 100
+        say(f"  mean loss {np.mean(losses):.6f}  median {np.median(losses):.6f}  "
+            f"spot {spots[0]:.2f} -> {spots[-1]:.2f}  mean |err| {np.mean(errs):.2f}%")
+    return calibrations

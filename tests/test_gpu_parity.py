@@ -1,0 +1,294 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) against the reference's golden vectors and
+the CPU oracle.  Run on the MI355X box with ``pytest -m gpu``.
+
+Tolerances (floating point, fp64):
+  * price parity bar:  |p_gpu - p_ref| <= 1e-6 |p_ref| + 1e-10
+  * fidelity target actually asserted on well-conditioned prices: 1e-10 relative
+  * losses: 1e-9 relative; FD gradients: conftest.fd_grad_tol with price noise 1e-13
+"""
+import numpy as np
+import pytest
+from scipy.optimize import minimize
+
+from conftest import fd_grad_tol, rel_close
+from oracle import dh_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+BAR_RTOL, BAR_ATOL = 1e-6, 1e-10
+FID_RTOL = 1e-10
+LOSS_RTOL = 1e-9
+EPS_PRICE = 1e-13
+
+
+@pytest.fixture(scope="module")
+def dh():
+    import dhcos
+    from dhcos import _native
+    if _native.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return dhcos
+
+
+def _mk(dhcos, e):
+    kw = dict(zip(("v01", "kappa1", "theta1", "sigma1", "rho1", "v02", "kappa2", "theta2",
+                   "sigma2", "rho2", "lambda_j", "mu_j", "sigma_j"), e["params"]))
+    return dhcos.DoubleHeston(S0=e["S0"], K=e["K"], T=e["T"], r=e["r"], q=e["q"],
+                              option_type=e["option_type"], **kw)
+
+
+# ---------------------------------------------------------------------------------------------
+# pricer
+# ---------------------------------------------------------------------------------------------
+def test_kat_pricing(dh, kat):
+    errs = []
+    for e in kat["prices"]:
+        m = _mk(dh, e)
+        if isinstance(e["price"], str):             # '' option type -> IndexError (Q3)
+            with pytest.raises(IndexError):
+                m.pricing(N=e["N"])
+            continue
+        got = m.pricing(N=e["N"])
+        assert isinstance(got, np.float64)
+        assert rel_close(got, e["price"], BAR_RTOL, BAR_ATOL), (e["tag"], got, e["price"])
+        if abs(e["price"]) > 1e-3:
+            errs.append(abs(got - e["price"]) / abs(e["price"]))
+            assert rel_close(got, e["price"], FID_RTOL, 0), (e["tag"], got, e["price"])
+    print("KAT max rel err", max(errs))
+
+
+def test_kat_truncation_cf_coeffs(dh, kat):
+    for e in kat["trunc"]:
+        m = dh.DoubleHeston(e["S0"], e["K"], e["T"], e["r"], *e["params"])
+        a, b = m.truncationRange()
+        assert rel_close([a, b], [e["a"], e["b"]], 1e-14, 1e-15).all()
+        a5, b5 = m.truncationRange(L=5)
+        assert rel_close([a5, b5], [e["a_L5"], e["b_L5"]], 1e-14, 1e-15).all()
+    for e in kat["cf"]:
+        m = dh.DoubleHeston(100.0, 100.0, 1.0, e["r"], *e["params"], q=e["q"])
+        c = m.characteristic_function(e["u"], e["tau"])
+        assert abs(c.real - e["re"]) <= 1e-13 * max(1.0, abs(e["re"]))
+        assert abs(c.imag - e["im"]) <= 1e-13 * max(1.0, abs(e["im"]))
+    m = dh.DoubleHeston(100.0, 100.0, 1.0, 0.05, *kat["cf"][0]["params"])
+    us = np.array([e["u"] for e in kat["cf"] if e["tau"] == 1.0])
+    arr = m.characteristic_function(us, 1.0)
+    assert arr.shape == us.shape
+    for e in kat["chipsi"]:
+        chi = m.chi_k(e["k"], e["c"], e["d"], e["a"], e["b"])
+        psi = m.psi_k(e["k"], e["c"], e["d"], e["a"], e["b"])
+        assert abs(chi - e["chi"]) <= 1e-13 * max(1.0, abs(e["chi"]))
+        assert abs(psi - e["psi"]) <= 1e-13 * max(1.0, abs(e["psi"]))
+
+
+def test_reference_sanity_section3(dh):
+    """tests/test_suite.py:196-262 restated: reasonableness and monotonicity."""
+    p = dict(v01=0.04, kappa1=2.0, theta1=0.04, sigma1=0.3, rho1=-0.5, v02=0.04, kappa2=1.5,
+             theta2=0.04, sigma2=0.2, rho2=-0.3, lambda_j=0.1, mu_j=0.0, sigma_j=0.1)
+    atm = dh.DoubleHeston(S0=100.0, K=100.0, T=1.0, r=0.05, option_type="call", **p).pricing(128)
+    assert 2.0 < atm < 15.0
+    ks = [dh.DoubleHeston(S0=100.0, K=k, T=1.0, r=0.05, option_type="call", **p).pricing(128)
+          for k in (90, 95, 100, 105, 110)]
+    assert np.sum(np.diff(ks) < 0) >= 3
+    ts = [dh.DoubleHeston(S0=100.0, K=100, T=t, r=0.05, option_type="call", **p).pricing(128)
+          for t in (0.25, 0.5, 1.0)]
+    assert np.all(np.diff(ts) > 0)
+    for S, K, T in ((100, 100, 0.25), (100, 100, 2.0), (100, 80, 1.0), (100, 120, 1.0)):
+        assert np.isfinite(dh.DoubleHeston(S0=S, K=K, T=T, r=0.05, option_type="call", **p).pricing(128))
+
+
+def test_random_grid_price_batch(dh, grid):
+    """All 1,600 golden grid rows in one paired launch per distinct N."""
+    got = np.empty_like(grid["price"])
+    for N in np.unique(grid["N"]):
+        sel = grid["N"] == N
+        got[sel] = dh.DoubleHeston.price_batch(grid["params"][sel], grid["S0"][sel], grid["K"][sel],
+                                               grid["T"][sel], grid["r"][sel],
+                                               grid["is_call"][sel].astype(bool), N=int(N),
+                                               q=grid["q"][sel])
+    want = grid["price"]
+    ok = rel_close(got, want, BAR_RTOL, BAR_ATOL) | (np.isnan(got) & np.isnan(want))
+    assert ok.all()
+    good = np.abs(want) > 1e-3
+    rel = np.abs(got[good] - want[good]) / np.abs(want[good])
+    print("grid max rel err", rel.max(), "median", np.median(rel))
+    assert rel.max() < FID_RTOL
+
+
+def _surface_case(seed, P, M, n_T, N, call_frac=0.5, S0=100.0, r=0.03):
+    rs = np.random.RandomState(seed)
+    lo = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
+    hi = np.array([0.08, 4.5, 0.065, 0.5, -0.4, 0.07, 1.2, 0.07, 0.35, -0.2, 0.25, -0.01, 0.12])
+    params = lo + (hi - lo) * rs.rand(P, 13)
+    Ts = np.linspace(0.1, 2.0, n_T)
+    T = Ts[rs.randint(n_T, size=M)]
+    K = S0 * rs.uniform(0.8, 1.2, M)
+    call = rs.rand(M) < call_frac
+    rec = np.empty((P, 16))
+    rec[:, :13], rec[:, 13], rec[:, 14], rec[:, 15] = params, S0, r, 0.0
+    return params, rec, K, T, call
+
+
+def test_surface_matches_oracle_and_pairs(dh):
+    """Surface mode (tiles shared across param sets, >256 options per maturity -> split tiles)."""
+    from dhcos import _native
+    params, rec, K, T, call = _surface_case(3, P=6, M=700, n_T=3, N=256)
+    ctx = _native.default_context()
+    surf = _native.Surface(ctx, K, T, call)
+    assert surf.n_tiles >= 4
+    out = surf.price(rec, N=256)
+    for p in range(params.shape[0]):
+        idx = np.arange(p, 700, 37)
+        want = O.price_many(params[p], 100.0, K[idx], T[idx], 0.03, call[idx], 256)
+        assert rel_close(out[p, idx], want, FID_RTOL, 1e-12).all()
+    # surface result == paired launch of the same (param set, option) pairs, bit for bit
+    pair = ctx.price_pairs(np.repeat(rec[:1], 700, axis=0), K, T, call, 256)
+    assert np.array_equal(pair, out[0])
+
+
+def test_batch_composition_and_order_invariance(dh):
+    """A param set's prices do not depend on its batch neighbours or the option order."""
+    from dhcos import _native
+    params, rec, K, T, call = _surface_case(5, P=14, M=1024, n_T=32, N=256)
+    ctx = _native.default_context()
+    s1 = _native.Surface(ctx, K, T, call)
+    full = s1.price(rec, N=256)
+    alone = s1.price(rec[7:8], N=256)
+    assert np.array_equal(full[7], alone[0])
+    perm = np.random.RandomState(0).permutation(1024)
+    s2 = _native.Surface(ctx, K[perm], T[perm], call[perm])
+    assert np.array_equal(s2.price(rec, N=256), full[:, perm])
+
+
+def test_put_call_parity_full_size(dh):
+    """C - P = S0 - K e^{-rT} (q = 0) on the C2-sized surface; COS error at N=256 is ~1e-9."""
+    from dhcos import _native
+    params, rec, K, T, _ = _surface_case(11, P=14, M=1024, n_T=32, N=256)
+    ctx = _native.default_context()
+    c = _native.Surface(ctx, K, T, np.ones(1024, np.int8)).price(rec, N=256)
+    p = _native.Surface(ctx, K, T, np.zeros(1024, np.int8)).price(rec, N=256)
+    pcp = c - p - (100.0 - K * np.exp(-0.03 * T))[None, :]
+    assert np.abs(pcp).max() < 1e-6
+
+
+def test_strike_pct_spot_mode(dh):
+    """Generator strikes K = K_rel * S0 / 100 formed on the device (synthetic_generator.py:125)."""
+    from dhcos import _native
+    params, rec, _, _, _ = _surface_case(2, P=5, M=1, n_T=1, N=128)
+    rec[:, 13] = [100.0, 97.3, 104.2, 88.8, 121.7]
+    Krel = np.tile(np.array([90, 95, 100, 105, 110], dtype=np.float64), 3)
+    T = np.repeat([0.25, 0.5, 1.0], 5)
+    out = _native.Surface(_native.default_context(), Krel, T, np.ones(15, np.int8),
+                          strike_mode=_native.STRIKE_PCT_SPOT).price(rec, N=128)
+    for p in range(5):
+        Kabs = Krel * rec[p, 13] / 100.0
+        want = O.price_many(params[p], rec[p, 13], Kabs, T, 0.03, True, 128)
+        assert rel_close(out[p], want, FID_RTOL, 1e-12).all()
+
+
+def test_empty_and_degenerate_sizes(dh):
+    from dhcos import _native
+    ctx = _native.default_context()
+    s = _native.Surface(ctx, [], [], [], [], )
+    assert s.price(np.zeros((3, 16)), 128).shape == (3, 0)
+    sse, bad, _ = s.loss_terms(np.zeros((2, 16)), 128)
+    assert np.all(sse == 0) and np.all(bad == 0)
+    assert ctx.price_pairs(np.zeros((0, 16)), [], [], [], 128).shape == (0,)
+    with pytest.raises(_native.NativeError):
+        ctx.price_pairs(np.zeros((1, 16)), [100.0], [1.0], [1], N=0)
+    with pytest.raises(_native.NativeError):
+        ctx.price_pairs(np.zeros((1, 16)), [100.0], [1.0], [1], N=_native.MAX_N + 1)
+
+
+# ---------------------------------------------------------------------------------------------
+# calibration objective
+# ---------------------------------------------------------------------------------------------
+def test_loss_values_and_semantics(dh, calib_golden):
+    g = calib_golden
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    for x, want in zip(g["guesses_seed0"], g["loss_at_guesses"]):
+        assert rel_close(cal.compute_loss(np.array(x)), want, LOSS_RTOL, 0)
+    for e in g["loss_random_x"]:
+        got = cal.compute_loss(np.array(e["x"]))
+        assert got == e["loss"] or rel_close(got, e["loss"], LOSS_RTOL, 0)
+    cal.n_calls = 0
+    assert cal.compute_loss(np.array(g["loss_absurd"]["x"])) == 1e10
+    assert cal.n_calls == 1
+    x0 = np.array(g["guesses_seed0"][0])
+    m0 = [dict(o) for o in g["test_market"][:3]]
+    m0[1]["price"] = 0.0
+    assert dh.DoubleHestonJumpCalibrator(100.0, 0.05, m0).compute_loss(x0) == np.inf
+    me = [dict(o) for o in g["test_market"][:3]]
+    me[2]["option_type"] = ""
+    assert dh.DoubleHestonJumpCalibrator(100.0, 0.05, me).compute_loss(x0) == 1e10
+    assert np.isnan(dh.DoubleHestonJumpCalibrator(100.0, 0.05, []).compute_loss(x0))
+    assert g["edge"]["zero_price"] == np.inf and g["edge"]["empty_type"] == 1e10
+
+
+def test_fd_batch_one_launch(dh, calib_golden):
+    g = calib_golden
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    for key in ("fd_guess0", "fd_guess2"):
+        e = g[key]
+        from dhcos.calibrator import fd_request_points
+        X, dx = fd_request_points(np.array(e["x0"]))
+        f = cal.loss_batch(X)
+        assert rel_close(f, e["f"], LOSS_RTOL, 0).all()
+        f0, grad = cal.compute_loss_and_grad(np.array(e["x0"]))
+        assert f0 == f[0]
+        assert np.all(np.abs(grad - np.array(e["g"])) <= fd_grad_tol(e["g"], f0, dx, EPS_PRICE))
+    assert abs(cal.compute_loss_and_grad(np.array(g["fd_guess0"]["x0"]))[1][8] - 80.0) < 0.01
+
+
+def test_reference_test_4_1_direct_minimize(dh, calib_golden):
+    """tests/test_suite.py:305-321: minimize(compute_loss) without jac, 294 evals, ABNORMAL."""
+    g = calib_golden["test_4_1"]
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, calib_golden["test_market"])
+    res = minimize(fun=cal.compute_loss, x0=cal.get_initial_guess(), method="L-BFGS-B",
+                   options={"maxiter": 200, "ftol": 1e-9})
+    assert res.nit == g["nit"] and res.nfev == g["nfev"] and res.message == g["message"]
+    assert rel_close(res.fun, g["fun"], 1e-8, 0)
+    assert res.fun * 100 < 1.0
+    assert cal.n_calls == g["n_calls"]
+
+
+def test_calibrate_seed0_matches_reference(dh, calib_golden):
+    """calibrate(300, 3) under np.random.seed(0): same winner, iterations and message."""
+    g = calib_golden
+    np.random.seed(0)
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    r = cal.calibrate(maxiter=300, multi_start=3)
+    want = g["calibrate_seed0"]
+    assert r.iterations == want["iterations"]
+    assert r.message == want["message"] and r.success == want["success"]
+    assert rel_close(r.final_loss, want["final_loss"], 1e-4, 0)
+    assert rel_close(r.model_prices, want["model_prices"], 1e-6, 0).all()
+    for k, v in want["parameters"].items():
+        assert rel_close(r.parameters[k], v, 1e-3, 1e-6), k
+    assert r.calibration_time is not None and r.calibration_time < want["seconds"]
+
+
+def test_lockstep_equals_sequential(dh, calib_golden):
+    g = calib_golden
+    from dhcos.calibrator import run_starts
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
+    a = run_starts(cal, x0s, 300, lockstep=True)
+    b = run_starts(cal, x0s, 300, lockstep=False)
+    for (ra, _), (rb, _), want in zip(a, b, g["calibrate_seed0_starts"]):
+        assert np.array_equal(ra.x, rb.x) and ra.fun == rb.fun and ra.nit == rb.nit
+        assert ra.nit == want["nit"] and ra.message == want["message"]
+        assert rel_close(ra.fun, want["fun"], 1e-4, 0)
+
+
+def test_generator_matches_reference(dh, gen_golden, tmp_path):
+    from dhcos import generate_synthetic_calibrations
+    np.random.seed(0)
+    res = generate_synthetic_calibrations(n_samples=len(gen_golden), save_path=str(tmp_path / "g.pkl"),
+                                          verbose=False)
+    for r, w in zip(res, gen_golden):
+        assert r.date == w["date"] and r.spot == w["spot"]
+        assert [r.parameters[k] for k in w["parameters"]] == list(w["parameters"].values())
+        assert [o["strike"] for o in r.market_options] == w["strikes"]
+        assert rel_close(r.model_prices, w["model_prices"], FID_RTOL, 0).all()
+        assert rel_close(r.market_prices, w["market_prices"], FID_RTOL, 0).all()
+        assert rel_close(r.final_loss, w["final_loss"], 1e-6, 0)

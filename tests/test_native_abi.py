@@ -1,0 +1,80 @@
+"""CPU-side checks of the C-ABI boundary: the library loads, exports every symbol declared in
+include/dhcos.h, the ctypes table matches the header, and compute entry points fail loudly
+(NativeError, no fallback) when no gfx950 device is present."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "dhcos.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(dh_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for f in ("dh_surface_price", "dh_surface_loss", "dh_price_pairs", "dh_cf", "dh_trunc_range",
+              "dh_cos_coeffs", "dh_surface_loss_dev", "dh_surface_price_dev"):
+        assert f in fns
+
+
+def test_library_exports_every_header_symbol():
+    from dhcos import _native
+    lib = _native.load()
+    for f in header_functions():
+        assert hasattr(lib, f), f
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dh_[a-z_]+)\b", out))
+    assert set(header_functions()) <= exported
+    assert set(_native.SIGNATURES) == set(header_functions())
+
+
+def test_library_is_gfx950_code_object():
+    """The fat binary carries a gfx950 (MI355X) code object and nothing else."""
+    from dhcos import _native
+    data = open(_native.LIB_PATH, "rb").read()
+    ids = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", data))
+    assert ids == {b"gfx950"}, ids
+
+
+def test_version_and_errors_without_device():
+    from dhcos import _native
+    lib = _native.load()
+    assert lib.dh_version() >= 1
+    if _native.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(_native.NativeError):
+        _native.Context(0)
+
+
+def test_product_path_fails_loudly_without_device():
+    from dhcos import DoubleHeston, NativeError, _native
+    if _native.device_count() > 0:
+        pytest.skip("a GPU is present")
+    dh = DoubleHeston(100, 100, 1.0, 0.05, 0.04, 2.0, 0.04, 0.3, -0.5, 0.04, 1.5, 0.04, 0.2, -0.3,
+                      0.5, -0.05, 0.1)
+    with pytest.raises(NativeError):
+        dh.pricing()
+
+
+def test_null_and_range_arguments_are_rejected():
+    """Argument validation happens before any device work."""
+    import ctypes as C
+    from dhcos import _native
+    lib = _native.load()
+    assert lib.dh_ctx_create(0, None) == -1
+    assert lib.dh_surface_price(None, None, None, 1, 128, 10.0, None) == -1
+    assert b"null" in lib.dh_last_error()
+    n = C.c_int32(-5)
+    lib.dh_device_count(C.byref(n))
+    assert n.value >= 0
+    assert np.int8(1) == 1
