@@ -38,9 +38,11 @@ from dhcos import _native                                      # noqa: E402
 from dhcos.calibrator import (DoubleHestonJumpCalibrator,      # noqa: E402
                               fd_request_points, x_to_model)
 
-# algorithmic work convention (DESIGN.md "Roofline"): fp64 flop-equivalents
-FLOP_CF = 716          # per unique characteristic-function evaluation (incl. e^{-iua} phase)
-FLOP_TERM = 120        # per (param set, option, COS term): payoff coefficients + accumulate
+# algorithmic work of the implemented algorithm, fp64 flop-equivalents (DESIGN.md "Roofline"):
+# add/mul = 1, fma = 2, exp/log/sin/cos/atan2 = 20, div/sqrt/hypot = 8 (SURVEY 8(d) weights)
+FLOP_TAB = 940         # per COS-table entry (p, T, k): CF (815) + phase, cos/sin(u(b-a)), T2..T4
+FLOP_TERM = 12         # per (param set, option, k >= 1): 3 fma + 1 complex rotation
+FLOP_OPT = 120         # per (param set, option): log(K/S0), exp, k = 0 term, constants
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector peak (spec)
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BYTES_PER_OPTION = 8 + 8 + 1 + 8 + 4   # K, T, is_call, mkt, perm read per (param set, option)
@@ -138,8 +140,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     os.environ["DHCOS_DEVICE"] = str(local)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: libdhcos launches on it and the HIP events time it
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
+    assert sptr, "expected a non-default HIP stream"
 
     opts, S0, r = make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
     M = len(opts)
@@ -153,15 +158,20 @@ def main():
     d_bad = torch.empty((K_ + W_, S), dtype=torch.int32, device=dev)
     N = cfg["N"]
 
+    ptrs = [(d_params[i].data_ptr(), d_sse[i].data_ptr(), d_bad[i].data_ptr())
+            for i in range(K_ + W_)]
+    loss_dev = surf.loss_dev
+
     def run(i):
-        surf.loss_dev(d_params[i].data_ptr(), S, d_sse[i].data_ptr(), d_bad[i].data_ptr(), N=N,
-                      stream=sptr)
+        pp, ps, pb = ptrs[i]
+        loss_dev(pp, S, ps, pb, N=N, stream=sptr)
 
     for i in range(W_):
         run(K_ + i)
-    # correctness spot check of one step against the host API (same kernel, host copies)
-    sse_h, bad_h, _ = surf.loss_terms(host[K_], N)
+    # correctness spot check of one step against the host API (same kernel, host copies);
+    # the context's scratch is shared, so drain the bench stream first
     torch.cuda.synchronize()
+    sse_h, bad_h, _ = surf.loss_terms(host[K_], N)
     assert np.array_equal(sse_h, d_sse[K_].cpu().numpy()), "device/host path mismatch"
 
     if world > 1:
@@ -181,32 +191,33 @@ def main():
     prices_per_step = S * M
     value = prices_per_step * K_ * world / dt
 
-    # ---- roofline of the dominant kernel (cos_price_kernel, loss mode), HIP events ----
-    n_tiles = surf.n_tiles
-    part_sse = torch.empty(S * n_tiles, dtype=torch.float64, device=dev)
-    part_bad = torch.empty(S * n_tiles, dtype=torch.int32, device=dev)
+    # ---- roofline of the dominant kernel (cos_price_kernel, loss mode; one launch per step) ----
     reps = max(20, min(K_, 200))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(reps)]
     for j, (e0, e1) in enumerate(evs):
         e0.record(stream)
-        surf.partials_dev(d_params[j % K_].data_ptr(), S, part_sse.data_ptr(), part_bad.data_ptr(),
-                          N=N, stream=sptr)
+        run(j % K_)
         e1.record(stream)
     torch.cuda.synchronize()
-    ker_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    ker_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
+    n_tiles = surf.n_tiles
     groups = len({o["maturity"] for o in opts})
-    flop = S * groups * N * FLOP_CF + S * M * N * FLOP_TERM
+    flop = S * groups * N * FLOP_TAB + S * M * (N - 1) * FLOP_TERM + S * M * FLOP_OPT
     achieved = flop / (ker_ms * 1e-3) / 1e12
-    alg_bytes = S * 16 * 8 + S * M * BYTES_PER_OPTION + S * n_tiles * 12
+    alg_bytes = S * 16 * 8 + S * M * BYTES_PER_OPTION + S * n_tiles * 12 + S * 12
+    survey_flop = S * groups * N * 716 + S * M * N * 120        # SURVEY 8(d) convention
     roofline = {"bound": "valu_fp64", "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4),
                 "traffic": pmc_traffic(args.config),
-                "kernel": "cos_price_kernel<256>", "kernel_ms": round(ker_ms, 5),
-                "flop_per_launch": flop, "alg_bytes_per_launch": alg_bytes,
+                "kernel": "cos_price_kernel<%d>" % (256 if N >= 256 else (128 if N >= 128 else 64)),
+                "kernel_ms": round(ker_ms, 5), "flop_per_launch": flop,
+                "alg_bytes_per_launch": alg_bytes,
                 "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
                         "peak_GBs": PEAK_HBM_GBS,
-                        "frac": alg_bytes / (ker_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}}
+                        "frac": alg_bytes / (ker_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
+                "survey_convention": {"flop_eq_per_launch": survey_flop,
+                                      "achieved_TFLOPs": survey_flop / (ker_ms * 1e-3) / 1e12}}
 
     # ---- calibrations/sec: one full single-start calibration of the same surface per rank ----
     calib = None
@@ -214,8 +225,9 @@ def main():
         c2 = DoubleHestonJumpCalibrator(S0, r, opts, N=N)
         if world > 1:
             dist.barrier()
+        np.random.seed(rank)
         t0 = time.perf_counter()
-        res = c2.calibrate(maxiter=300, multi_start=1)
+        res = c2.calibrate(maxiter=300, multi_start=3)   # reference defaults, lockstep starts
         tc = time.perf_counter() - t0
         if world > 1:
             tt = torch.tensor([tc], dtype=torch.float64, device=dev)
@@ -223,7 +235,8 @@ def main():
             tc = float(tt.item())
         calib = {"calibrations_per_sec": world / tc, "seconds": tc, "iterations": int(res.iterations),
                  "final_loss": float(res.final_loss), "message": res.message,
-                 "fd_requests": int(c2.n_calls // 14)}
+                 "lockstep_launches": int(getattr(c2, "lockstep_launches", 0)),
+                 "calibrate": "calibrate(maxiter=300, multi_start=3), np.random.seed(rank)"}
 
     if rank == 0:
         line = {

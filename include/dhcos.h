@@ -62,6 +62,13 @@ int dh_ctx_destroy(dh_ctx* ctx);
 int dh_ctx_synchronize(dh_ctx* ctx);
 /* The HIP stream the context launches on (hipStream_t as void*). */
 void* dh_ctx_stream(dh_ctx* ctx);
+/* Validation mode: when on, every option is priced by the per-term path in the reference's
+ * operation order (own CF and sincos per COS term) instead of the shared-table fast path.   */
+int dh_ctx_set_exact(dh_ctx* ctx, int on);
+/* Diagnostics (only in the DH_STAMPS build, `make stamps`; the production library returns
+ * DH_E_ARG): record per-block s_memtime phase stamps of the COS kernel, read the last launch's. */
+int dh_ctx_debug_stamps(dh_ctx* ctx, int on);
+int dh_ctx_read_stamps(dh_ctx* ctx, unsigned long long* out, int64_t cap, int64_t* n);
 
 /* ---- option surfaces ---------------------------------------------------------------------- */
 /* Upload an option set once.  Options are grouped by exact maturity on the host; groups are cut
@@ -91,19 +98,14 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
                     double L, double* sse, int32_t* n_bad, double* prices);
 
 /* Device-pointer variants: params/out/sse/n_bad are device pointers; enqueue on `stream`
- * (hipStream_t; NULL = context stream).  No synchronisation, no allocation after warm-up.     */
+ * (hipStream_t; NULL = context stream).  No synchronisation, no allocation after warm-up.
+ * dh_surface_loss_dev is ONE kernel launch (the last task of each param set finalises its sum).
+ * Launches through one context share its scratch: issue them on one stream at a time.       */
 int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int64_t P,
                          int N, double L, double* d_out, void* stream);
 int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S, int N,
                         double L, double* d_sse, int32_t* d_n_bad, double* d_prices,
                         void* stream);
-
-/* First stage of dh_surface_loss_dev only (the COS kernel in loss mode): writes one
- * (sse, n_bad) partial per (param set, tile) into d_part_sse / d_part_bad [S * n_tiles].
- * Exposed so a caller (bench.py) can time the dominant kernel alone.                         */
-int dh_surface_partials_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S,
-                            int N, double L, double* d_part_sse, int32_t* d_part_bad,
-                            void* stream);
 
 /* ---- paired pricing: option i under param set i ------------------------------------------- */
 /* out[i] = price of (K[i], T[i], is_call[i]) under params[i]; replaces a loop of single

@@ -52,15 +52,118 @@ __device__ __forceinline__ cplx csqrt_p(cplx z) {
     return {fabs(0.5 * (y / s)), copysign(s, y)};
 }
 
+// sin and cos of one argument: 3-part Cody-Waite reduction by pi/2 with FMA, then the fdlibm
+// kernel polynomials on [-pi/4, pi/4] (coefficients of __kernel_sin / __kernel_cos).  Max error
+// ~2 ulp for |x| < 2^20 (every argument on this path is bounded by N pi plus the CF phases);
+// accuracy degrades gracefully beyond, and non-finite x gives NaN like libm.  Replaces ocml's
+// sincos, whose inlined Payne-Hanek branch costs ~100 VGPRs per call site.
+__device__ __forceinline__ void dsincos(double x, double* sp, double* cp) {
+    const double q = rint(x * 6.36619772367581382433e-01);           // x * 2/pi
+    double r = fma(-q, 1.57079632679489655800e+00, x);                 // pi/2, 3 parts
+    r = fma(-q, 6.12323399573676588613e-17, r);
+    r = fma(-q, -1.49738490485916983089e-33, r);
+    const double z = r * r;
+    const double ps = -1.66666666666666324348e-01 +
+        z * (8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 +
+        z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 +
+        z * 1.58969099521155010221e-10))));
+    const double s = fma(r * z, ps, r);
+    const double pc = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 +
+        z * (2.48015872894767294178e-05 + z * (-2.75573143513906633035e-07 +
+        z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + z * pc);
+    const double qm = q - 4.0 * floor(q * 0.25);                       // quadrant in {0,1,2,3}
+    const bool swap = (qm == 1.0) || (qm == 3.0);
+    const double s1 = swap ? c : s, c1 = swap ? s : c;
+    *sp = (qm >= 2.0) ? -s1 : s1;
+    *cp = (qm == 1.0 || qm == 2.0) ? -c1 : c1;
+}
+
 __device__ __forceinline__ cplx cexp_(cplx z) {
     double s, c;
-    sincos(z.im, &s, &c);
+    dsincos(z.im, &s, &c);
     const double e = exp(z.re);
     return {e * c, e * s};
 }
 
 // Principal log: arg in (-pi, pi].
 __device__ __forceinline__ cplx clog_(cplx z) { return {log(hypot(z.re, z.im)), atan2(z.im, z.re)}; }
+
+// ---- lean fp64 elementary functions for the hot kernel (fdlibm algorithms, < 1-2 ulp) -------
+// ocml's fp64 log / atan2 cost ~90-100 VALU instructions each (double-double internals); these
+// restate fdlibm's e_log.c / s_atan.c / e_atan2.c with select-based interval reduction.
+
+// log(x) for any x: x = 2^k (1 + f), sqrt(1/2) <= 1 + f < sqrt(2), s = f / (2 + f).
+__device__ __forceinline__ double dlog(double x) {
+    int k;
+    double m = frexp(x, &k);                         // m in [0.5, 1)
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? 2.0 * m : m;
+    k = lo ? k - 1 : k;
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double z = s * s, w = z * z;
+    const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 +
+                      w * 1.531383769920937332e-01));
+    const double t2 = z * (6.666666666666735130e-01 + w * (2.857142874366239149e-01 +
+                      w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    const double R = t2 + t1;
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)k;
+    const double r = dk * 6.93147180369123816490e-01 -
+                     ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+    // special values: log(0) = -inf, log(x < 0) = NaN, log(inf) = inf, log(NaN) = NaN
+    if (!(x > 0.0) || isinf(x)) return (x == 0.0) ? -INFINITY : (x > 0.0 ? x : NAN + x);
+    return r;
+}
+
+// atan(t) for t >= 0 (fdlibm s_atan.c), interval reduction by selects and one division.
+__device__ __forceinline__ double datan_pos(double t) {
+    // id: -1 (t < 0.4375), 0 (< 0.6875), 1 (< 1.1875), 2 (< 2.4375), 3 (otherwise)
+    const bool r0 = t >= 0.4375, r1 = t >= 0.6875, r2 = t >= 1.1875, r3 = t >= 2.4375;
+    // t' = (a t + b) / (c t + d)
+    const double a = r3 ? 0.0 : (r2 ? 1.0 : (r1 ? 1.0 : (r0 ? 2.0 : 1.0)));
+    const double b = r3 ? -1.0 : (r2 ? -1.5 : (r1 ? -1.0 : (r0 ? -1.0 : 0.0)));
+    const double c = r3 ? 1.0 : (r2 ? 1.5 : (r1 ? 1.0 : (r0 ? 1.0 : 0.0)));
+    const double d = r3 ? 0.0 : (r2 ? 1.0 : (r1 ? 1.0 : (r0 ? 2.0 : 1.0)));
+    const double x = fma(a, t, b) / fma(c, t, d);
+    const double hi = r3 ? 1.57079632679489655800e+00 : (r2 ? 9.82793723247329054082e-01 :
+                      (r1 ? 7.85398163397448278999e-01 : 4.63647609000806093515e-01));
+    const double lo = r3 ? 6.12323399573676588613e-17 : (r2 ? 1.39033110312309984516e-17 :
+                      (r1 ? 3.06161699786838301793e-17 : 2.26987774529616870924e-17));
+    const double z = x * x, w = z * z;
+    const double s1 = z * (3.33333333333329318027e-01 + w * (1.42857142725034663711e-01 +
+                      w * (9.09088713343650656196e-02 + w * (6.66107313738753120669e-02 +
+                      w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
+    const double s2 = w * (-1.99999999998764832476e-01 + w * (-1.11111104054623557880e-01 +
+                      w * (-7.69187620504482999495e-02 + w * (-5.83357013379057348645e-02 +
+                      w * -3.65315727442169155270e-02))));
+    const double small = x - x * (s1 + s2);
+    const double big = hi - ((x * (s1 + s2) - lo) - x);
+    return r0 ? big : small;
+}
+
+// atan2(y, x), principal value in (-pi, pi] (fdlibm e_atan2.c quadrant logic) for finite x, y.
+__device__ __forceinline__ double datan2(double y, double x) {
+    const double ax = fabs(x), ay = fabs(y);
+    const double z = datan_pos(ay / ax);             // y/x = +-inf and 0/0 handled below
+    const double pi = 3.1415926535897931160e+00, pi_lo = 1.2246467991473531772e-16;
+    double r = (x >= 0.0) ? z : pi - (z - pi_lo);
+    r = (ay == 0.0 && x >= 0.0) ? 0.0 : r;            // atan2(+-0, x >= 0) = +-0
+    r = (ay == 0.0 && x < 0.0) ? pi : r;              // atan2(+-0, x < 0) = +-pi
+    r = (ax == 0.0 && ay != 0.0) ? 1.57079632679489655800e+00 : r;
+    r = copysign(r, y);
+    return (isnan(x) || isnan(y)) ? x + y : r;
+}
+
+// z1 / z2 through one fp64 reciprocal of |z2|^2 (no Smith scaling: |z2| on this path stays far
+// from the fp64 over/underflow thresholds).
+__device__ __forceinline__ cplx cdiv_rcp(cplx a, cplx b) {
+    const double inv = 1.0 / fma(b.re, b.re, b.im * b.im);
+    return {(a.re * b.re + a.im * b.im) * inv, (a.im * b.re - a.re * b.im) * inv};
+}
 
 // Param-set record (DH_PARAM_STRIDE = 16 doubles), double_heston.py:26-46 argument order.
 struct Params {
@@ -110,13 +213,104 @@ __device__ __forceinline__ cplx cf_eval(const Params& P, double u, double tau) {
     return cmul(cexp_(ex), jump);                                     // :94-96
 }
 
+// ---- fast CF for the COS table: exponent form ----------------------------------------------
+// phi(u) = exp(E) with E = A + B1 v01 + B2 v02 + lambda tau (e^{i u mu - sj^2 u^2/2} - 1); the
+// table only needs Re(phi e^{-i u a}) = e^{Re E} cos(Im E - u a), so the three final complex
+// exponentials and two complex products of cf_eval collapse into one exp and one cos.  Per factor,
+// g = (beta - d)/(beta + d) is eliminated algebraically:
+//   (1 - e)/(1 - g e) = (1 - e)(beta + d) / D,   (1 - g e)/(1 - g) = D / (2 d),
+//   D = (beta + d) - (beta - d) e,  e = exp(-d tau)
+// which is the same 'little Heston trap' quantity, with two complex divisions instead of three.
+struct FactorC {
+    double kap, rs, s2, inv_s2, coef, v0;   // kappa, rho sigma, sigma^2, 1/sigma^2, k th/s^2, v0
+};
+
+__device__ __forceinline__ FactorC factor_consts(double v0, double kap, double th, double sig,
+                                                 double rho) {
+    FactorC F;
+    F.kap = kap;
+    F.rs = rho * sig;
+    F.s2 = sig * sig;
+    F.inv_s2 = 1.0 / F.s2;
+    F.coef = (kap * th) / F.s2;
+    F.v0 = v0;
+    return F;
+}
+
+__device__ __forceinline__ void factor_exponent(const FactorC& F, double u, double tau, cplx& E) {
+    const cplx beta = {F.kap, -(F.rs * u)};
+    const double s2u = F.s2 * u;
+    const cplx dd = {fma(beta.re, beta.re, -beta.im * beta.im) + s2u * u,
+                     2.0 * beta.re * beta.im + s2u};
+    // principal sqrt
+    const double h = sqrt(fma(dd.re, dd.re, dd.im * dd.im));
+    double dre, dim;
+    if (dd.re > 0.0) {
+        dre = sqrt(0.5 * (h + dd.re));
+        dim = 0.5 * dd.im / dre;
+    } else {
+        const double t = sqrt(0.5 * (h - dd.re));
+        dre = fabs(0.5 * dd.im / t);
+        dim = copysign(t, dd.im);
+    }
+    const cplx bm = {beta.re - dre, beta.im - dim};
+    const cplx bp = {beta.re + dre, beta.im + dim};
+    double es, ec;
+    dsincos(-dim * tau, &es, &ec);
+    const double em = exp(-dre * tau);
+    const cplx e = {em * ec, em * es};
+    const cplx D = {bp.re - (bm.re * e.re - bm.im * e.im), bp.im - (bm.re * e.im + bm.im * e.re)};
+    const cplx ome = {1.0 - e.re, -e.im};
+    const cplx num = cmul(cscale(bm, F.inv_s2), cmul(ome, bp));
+    const cplx B = cdiv_rcp(num, D);
+    const cplx Q = cdiv_rcp(D, {2.0 * dre, 2.0 * dim});
+    const double lq_re = 0.5 * dlog(fma(Q.re, Q.re, Q.im * Q.im));
+    const double lq_im = datan2(Q.im, Q.re);
+    E.re += F.coef * (bm.re * tau - 2.0 * lq_re) + B.re * F.v0;
+    E.im += F.coef * (bm.im * tau - 2.0 * lq_im) + B.im * F.v0;
+}
+
+// Per-(param set, T) constants of the fast CF.
+struct CfConsts {
+    FactorC f1, f2;
+    double drift;      // (r - q - lambda (e^{mu + sj^2/2} - 1)) tau
+    double half_sj2, muj, lt;
+};
+
+__device__ __forceinline__ CfConsts cf_consts(const Params& P, double tau) {
+    CfConsts C;
+    C.f1 = factor_consts(P.v01, P.k1, P.t1, P.s1, P.r1);
+    C.f2 = factor_consts(P.v02, P.k2, P.t2, P.s2, P.r2);
+    const double comp = exp(P.muj + 0.5 * (P.sj * P.sj)) - 1.0;
+    C.drift = (P.r - P.q - P.lam * comp) * tau;
+    C.half_sj2 = 0.5 * (P.sj * P.sj);
+    C.muj = P.muj;
+    C.lt = P.lam * tau;
+    return C;
+}
+
+// Re(phi(u) e^{-i u a}) via the exponent form.
+__device__ __forceinline__ double cf_phase_re(const CfConsts& C, double u, double tau, double a) {
+    cplx E = {0.0, C.drift * u};
+    factor_exponent(C.f1, u, tau, E);
+    factor_exponent(C.f2, u, tau, E);
+    double js, jc;
+    dsincos(u * C.muj, &js, &jc);
+    const double jm = exp(-(C.half_sj2 * (u * u)));
+    E.re += C.lt * (jm * jc - 1.0);
+    E.im += C.lt * (jm * js);
+    double ps, pc;
+    dsincos(E.im - u * a, &ps, &pc);
+    return exp(E.re) * pc;
+}
+
 // First two cumulants of one factor (double_heston.py:101-118).  Q1: c1 includes r*tau.
 __device__ __forceinline__ void factor_cumulants(double tau, double r, double v0, double lm,
                                                  double vb, double vv, double rho, double& c1,
                                                  double& c2) {
     const double ek = exp(-lm * tau);
     c1 = r * tau + (1.0 - ek) * (vb - v0) / (2.0 * lm) - vb * tau / 2.0;
-    const double lm2 = lm * lm, lm3 = pow(lm, 3.0), vv2 = vv * vv;
+    const double lm2 = lm * lm, lm3 = lm2 * lm, vv2 = vv * vv;   // np.power(lm, 3) ~ lm*lm*lm
     c2 = 1.0 / (8.0 * lm3) *
          (vv * tau * lm * ek * (v0 - vb) * (8.0 * lm * rho - 4.0 * vv) +
           lm * rho * vv * (1.0 - ek) * (16.0 * vb - 8.0 * v0) +
@@ -148,8 +342,8 @@ __device__ __forceinline__ void cos_coeffs(int k, double c, double d, double a, 
     }
     const double u = k * kPi / (b - a);
     double sd, cd, sc, cc;
-    sincos(u * (d - a), &sd, &cd);
-    sincos(u * (c - a), &sc, &cc);
+    dsincos(u * (d - a), &sd, &cd);
+    dsincos(u * (c - a), &sc, &cc);
     const double ed = exp(d), ec = exp(c);
     chi = (1.0 / (1.0 + u * u)) * (cd * ed - cc * ec + u * sd * ed - u * sc * ec);
     psi = (1.0 / u) * (sd - sc);

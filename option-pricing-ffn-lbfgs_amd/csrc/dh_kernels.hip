@@ -1,26 +1,29 @@
 // dh_kernels.hip -- gfx950 kernels of the COS pricing / calibration-objective hot path.
 //
-// Work decomposition (see DESIGN.md "Kernels"):
-//   task  = (param set p, tile) where a tile is <= 256 options sharing one maturity T.
-//   block = 256 threads = 256/TPT tasks of TPT threads each (TPT in {64,128,256}).
-//   phase 1: the task's threads build the per-(p, T) COS table in LDS for k = 0..N-1:
-//            u_k, w_k = Re(phi(u_k) e^{-i u_k a}) * 2/(b-a) (k=0 halved), cos/sin(u_k (b-a)),
-//            1/(1+u_k^2), 1/u_k                    (double_heston.py:163-168,187-188)
-//   phase 2: each option is reduced by a G-lane subgroup (G = power of two, G*options ~ TPT);
-//            lane j owns a contiguous k-range, evaluates the payoff coefficients chi/psi
-//            (double_heston.py:141-158,176-185) against the shared table, and the subgroup is
-//            reduced with DPP butterflies (__shfl_xor).  Options whose truncation range is widened
-//            by the log-strike clamp (double_heston.py:135-137) evaluate their own CF per term.
-//   phase 3: (loss mode) the task's relative squared errors and invalid-price count are reduced
-//            in a fixed order into one partial per task; dh_loss_finalize sums the partials of each
-//            param set in tile order.  No atomics: results are bitwise reproducible and do not
-//            depend on how many param sets share a launch.
+// Work decomposition (DESIGN.md "Kernels"):
+//   task  = (param set p, tile); a tile is <= 256 options sharing one maturity T.
+//   block = 256 threads = 256/TPT tasks of TPT threads (TPT in {64,128,256}, chosen from N).
+//   phase 1  (CF table, once per (p, T)): the task's threads evaluate phi(u_k) for k < N and
+//            fold it with the k-only parts of the payoff coefficients (double_heston.py:141-158,
+//            176-190) into three LDS columns T2/T3/T4 plus three k-sums (call / put constants).
+//   phase 2  (per option): the COS sum splits into option-independent constants and two
+//            angle sums  S2 = sum_k T2_k cos(k th) + T3_k sin(k th),  S4 = sum_k T4_k sin(k th),
+//            th = pi (log(K/S0) - a) / (b - a).  A G-lane subgroup walks k interleaved (lane j:
+//            k = 1 + j, 1 + j + G, ...), advancing the angle by a complex rotation e^{i G th}
+//            with an exact sincos re-anchor every 64 steps, then reduces with DPP butterflies.
+//            Options whose [a, b] is widened by the log-strike clamp (double_heston.py:135-137)
+//            are queued and priced after a rebuild of the table on their own range (same code,
+//            block-uniform trip count).  Validation ("exact") mode instead runs cos_exact_kernel:
+//            per-term CF + sincos in the reference's operation order, one wave per option.
+//   phase 3  (loss mode): per-task fixed-order partial of sum rel^2 and #invalid; the last task
+//            of a param set to finish (agent-scope counter, release/acquire) sums the partials
+//            in tile order.  One launch per request, no float atomics, bitwise reproducible and
+//            independent of how many param sets share the launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
-#include <mutex>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -35,7 +38,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kTileMax = 256;
-constexpr int kTabFields = 6;  // u, w, cos(u(b-a)), sin(u(b-a)), 1/(1+u^2), 1/u
+constexpr int kAnchor = 64;       // exact sincos re-anchor period of the angle recurrence
 
 struct PriceArgs {
     const double* prm;      // [P][16]
@@ -49,57 +52,345 @@ struct PriceArgs {
     int n_tiles;
     int paired;             // option i under param set i, one option per task
     int strike_mode;
+    int exact;              // validation mode (host routes to cos_exact_kernel)
+    int M;                  // options in the (sorted) option arrays
     int N;
     double L;
-    double* out;            // prices or null
+    double* out;            // prices [P*out_stride] or null
     int64_t out_stride;     // M (surface) or 0 (paired)
-    double* part_sse;       // [P*n_tiles] or null
+    double* part_sse;       // loss mode: [P*n_tiles] partials, else null
     int* part_bad;          // [P*n_tiles]
+    unsigned* counter;      // [P] arrival counters (zero between launches)
+    double* sse;            // [P] final sums (loss mode)
+    int* n_bad;             // [P]
+    unsigned long long* stamps;   // diagnostic builds (DH_STAMPS) only: [blocks][kStamps]
 };
 
-// ----------------------------------------------------------------------------------------------
-// one COS term for k >= 1:  w_k * V_k where V_k is the payoff coefficient of the option.
-// call: c = xK, d = b;  put: c = a, d = xK.  sx/cx = sin/cos(u (xK - a)); sb/cb = sin/cos(u(b-a)).
-// ----------------------------------------------------------------------------------------------
-__device__ __forceinline__ double payoff_coeff(bool is_call, double u, double i1, double iu,
-                                               double cb, double sb, double cx, double sx,
-                                               double eb, double ea, double exK, double S0,
-                                               double K) {
-    double chi, psi;
-    if (is_call) {  // d = b, c = xK   (double_heston.py:176-179)
-        chi = i1 * (cb * eb - cx * exK + u * sb * eb - u * sx * exK);
-        psi = iu * (sb - sx);
-        return S0 * chi - K * psi;
-    }
-    // put: d = xK, c = a: cos(u*0) = 1, sin(u*0) = 0 (double_heston.py:182-185)
-    // (the reference's "- u*sin(0)*e^a" and "- sin(0)" terms are exact zeros and are dropped)
-    chi = i1 * (cx * exK - ea + u * sx * exK);
-    psi = iu * sx;
-    return K * psi - S0 * chi;
+// In-kernel phase stamps, compiled only into the diagnostic build (make stamps): lane 0 of each
+// block writes s_memtime at the phase boundaries and s_memrealtime at start/end.
+constexpr int kStamps = 8;
+#ifdef DH_STAMPS
+#define DH_STAMP(A, i)                                                                     \
+    do {                                                                                   \
+        if ((A).stamps && threadIdx.x == 0) {                                              \
+            unsigned long long _t;                                                         \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+            (A).stamps[(size_t)blockIdx.x * kStamps + (i)] = _t;                          \
+        }                                                                                  \
+    } while (0)
+#define DH_RSTAMP(A, i)                                                                    \
+    do {                                                                                   \
+        if ((A).stamps && threadIdx.x == 0)                                                \
+            (A).stamps[(size_t)blockIdx.x * kStamps + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define DH_STAMP(A, i) do {} while (0)
+#define DH_RSTAMP(A, i) do {} while (0)
+#endif
+
+__host__ __device__ constexpr int task_lds_doubles(int N, int tpt) {
+    // (T2,T3)[N] u[N] T4[N] | reduction [4][waves] | K, mkt, sse, bad [kTileMax] |
+    // call, perm, clamp list [kTileMax] ints + count (rounded to whole 16-B pairs)
+    return 4 * N + 4 * (tpt / 64) + 4 * kTileMax + ((3 * kTileMax + 4) / 2 + 1) / 2 * 2;
 }
 
+__device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int col, double mk,
+                                             int oi, double price, double* lsse, double* lbad) {
+    if (A.out) A.out[p * A.out_stride + col] = price;
+    if (A.part_sse) {
+        const double rel = (price - mk) / mk;
+        lsse[oi] = rel * rel;
+        // lbfgs_calibrator.py:152: NaN, inf or <= 0 is invalid
+        lbad[oi] = (isnan(price) || isinf(price) || price <= 0.0) ? 1.0 : 0.0;
+    }
+}
+
+// Fixed-order loss partial of one task (wave 0 of the task).  Hand-off to the last task of param
+// set p without fences (MI355X_MICROARCH.md, "Valid forms", first table row): the storing lane
+// writes its partial with agent-scope (sc1, write-through) stores, drains them with
+// s_waitcnt vmcnt(0), then adds to p's counter; the lane whose add returns n_tiles - 1 reads every
+// partial of p with sc1 loads, sums them in tile order and resets the counter for the next launch.
+__device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t task, int nopt,
+                                          int t, const double* lsse, const double* lbad) {
+    double s = 0.0, f = 0.0;
+    for (int i = t; i < nopt; i += 64) {
+        s += lsse[i];
+        f += lbad[i];
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+        s += __shfl_xor(s, off, 64);
+        f += __shfl_xor(f, off, 64);
+    }
+    const int64_t base_i = p * A.n_tiles;
+    unsigned old = 0;
+    if (t == 0) {
+        __hip_atomic_store(&A.part_sse[task], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&A.part_bad[task], (int)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        old = __hip_atomic_fetch_add(&A.counter[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    old = __shfl(old, 0, 64);
+    if (old != (unsigned)A.n_tiles - 1u) return;
+    // last arriver: the whole wave reads the partials of p (lane-strided, sc1), fixed order
+    double acc = 0.0, bad = 0.0;
+    for (int j = t; j < A.n_tiles; j += 64) {
+        acc += __hip_atomic_load(&A.part_sse[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bad += __hip_atomic_load(&A.part_bad[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+        acc += __shfl_xor(acc, off, 64);
+        bad += __shfl_xor(bad, off, 64);
+    }
+    if (t == 0) {
+        A.sse[p] = acc;
+        A.n_bad[p] = (int)bad;
+        __hip_atomic_store(&A.counter[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// exact per-term path (validation mode): own truncation range, own u grid, CF per term, the
+// reference's operation order (double_heston.py:160-192).  Lane share of sum_k' Re(phi e^{-iua}) V_k.
+// ----------------------------------------------------------------------------------------------
+__device__ __forceinline__ double exact_term_sum(const Params& P, double T, double K, double xK,
+                                                 double a, double b, bool is_call, int k_first,
+                                                 int k_step, int N) {
+    const double ba = b - a;
+    const double scale = 2.0 / ba;
+    double acc = 0.0;
+    for (int k = k_first; k < N; k += k_step) {
+        const double u = k * dh::kPi / ba;
+        const cplx phi = dh::cf_eval(P, u, T);
+        double sa, ca;
+        dh::dsincos(u * a, &sa, &ca);
+        const double re = phi.re * ca + phi.im * sa;       // Re(phi exp(-i u a))
+        double chi, psi;
+        if (is_call) dh::cos_coeffs(k, xK, b, a, b, chi, psi);
+        else dh::cos_coeffs(k, a, xK, a, b, chi, psi);
+        const double V = is_call ? scale * (P.S0 * chi - K * psi) : scale * (K * psi - P.S0 * chi);
+        double term = re * V;
+        if (k == 0) term *= 0.5;
+        acc += term;
+    }
+    return acc;
+}
+
+__device__ __forceinline__ double option_strike(const PriceArgs& A, int m, double S0) {
+    const double Kin = A.K[m];
+    return (A.strike_mode == DH_STRIKE_PCT_SPOT) ? Kin * S0 / 100.0 : Kin;
+}
+
+// Validation kernel: one wave per (param set, option); prices only (loss via loss_from_prices).
+__global__ __launch_bounds__(kBlock) void cos_exact_kernel(PriceArgs A, int M, double* prices) {
+    const int64_t item = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t n_items = A.paired ? A.P : A.P * (int64_t)M;
+    if (item >= n_items) return;                       // whole wave exits together
+    const int64_t p = A.paired ? item : item / M;
+    const int m = A.paired ? (int)item : (int)(item % M);
+    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
+    const double T = A.T[m];
+    const double K = option_strike(A, m, P.S0);
+    const bool is_call = A.call[m] != 0;
+    const double xK = log(K / P.S0);
+    double a0, b0;
+    dh::trunc_unclamped(P, T, A.L, a0, b0);
+    const double a = (xK - 0.1 < a0) ? xK - 0.1 : a0;   // Python min/max semantics (:136-137)
+    const double b = (xK + 0.1 > b0) ? xK + 0.1 : b0;
+    double acc = exact_term_sum(P, T, K, xK, a, b, is_call, lane, 64, A.N);
+    for (int off = 1; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) {
+        const double price = exp(-P.r * T) * acc;
+        if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
+        if (prices) prices[p * M + m] = price;
+    }
+}
+
+// Loss sums from a [P][M] price buffer (validation mode): one wave per param set, fixed order.
+__global__ void loss_from_prices_kernel(const double* __restrict__ prices,
+                                        const double* __restrict__ mkt, int M, int S,
+                                        double* __restrict__ sse, int* __restrict__ n_bad) {
+    const int s = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    if (s >= S) return;
+    double acc = 0.0, bad = 0.0;
+    for (int m = lane; m < M; m += 64) {
+        const double pr = prices[(int64_t)s * M + m];
+        const double rel = (pr - mkt[m]) / mkt[m];
+        acc += rel * rel;
+        bad += (isnan(pr) || isinf(pr) || pr <= 0.0) ? 1.0 : 0.0;
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+        acc += __shfl_xor(acc, off, 64);
+        bad += __shfl_xor(bad, off, 64);
+    }
+    if (lane == 0) {
+        sse[s] = acc;
+        n_bad[s] = (int)bad;
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// table build: COS table of (p, T, [a, b]) into LDS + the four k-sums, reduced in fixed order.
+// w_k = Re(phi(u_k) e^{-i u_k a}) 2/(b-a);  T2 = w S0/(1+u^2), T3 = T2 u, T4 = w/u   (k >= 1)
+// c0 = sum T2 e^b (cos(u(b-a)) + u sin(u(b-a)))   (call constant)
+// c1 = sum T4 sin(u(b-a))                          (call constant, times K)
+// c5 = sum T2 e^a                                  (put constant)
+// w0 = w_0 / 2                                     (k = 0 term weight)
+// Must be reached by every thread of the block (contains a barrier).
+// ----------------------------------------------------------------------------------------------
+struct Consts {
+    double c0, c1, c5, w0, eb, ea;
+};
+
 template <int TPT>
-__global__ __launch_bounds__(kBlock) void cos_price_kernel(PriceArgs A) {
+__device__ __forceinline__ Consts build_table(const Params& P, double T, double a, double b,
+                                              bool work, int N, int t, double* tu, double2* t23,
+                                              double* t4, double* red) {
+    constexpr int kWaves = TPT / 64;
+    const int lane = threadIdx.x & 63;
+    const int wv = t >> 6;
+    const double ba = b - a;
+    const double scale = 2.0 / ba;
+    const double eb = exp(b), ea = exp(a);
+    const dh::CfConsts CC = dh::cf_consts(P, T);
+    double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
+    if (work) {
+        for (int k = t; k < N; k += TPT) {
+            const double u = k * dh::kPi / ba;
+            const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+            if (k == 0) {
+                w0 = 0.5 * w;
+                continue;
+            }
+            double sb, cb;
+            dh::dsincos(u * ba, &sb, &cb);
+            const double i1 = 1.0 / (1.0 + u * u);
+            const double T2 = w * P.S0 * i1;
+            const double T4 = w * (1.0 / u);
+            tu[k] = u;
+            t23[k] = make_double2(T2, T2 * u);
+            t4[k] = T4;
+            c0 += T2 * eb * (cb + u * sb);
+            c1 += T4 * sb;
+            c5 += T2 * ea;
+        }
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+        c0 += __shfl_xor(c0, off, 64);
+        c1 += __shfl_xor(c1, off, 64);
+        c5 += __shfl_xor(c5, off, 64);
+        w0 += __shfl_xor(w0, off, 64);
+    }
+    if (lane == 0) {
+        red[0 * kWaves + wv] = c0;
+        red[1 * kWaves + wv] = c1;
+        red[2 * kWaves + wv] = c5;
+        red[3 * kWaves + wv] = w0;
+    }
+    __syncthreads();
+    Consts C{0.0, 0.0, 0.0, 0.0, eb, ea};
+    for (int i = 0; i < kWaves; ++i) {
+        C.c0 += red[0 * kWaves + i];
+        C.c1 += red[1 * kWaves + i];
+        C.c5 += red[2 * kWaves + i];
+        C.w0 += red[3 * kWaves + i];
+    }
+    return C;
+}
+
+// sum' of one option from the table constants and its angle sums (k = 0 term:
+// chi_0 = e^d - e^c, psi_0 = d - c, double_heston.py:142-143,154-155).
+__device__ __forceinline__ double option_sum(const Consts& C, bool is_call, double S0, double K,
+                                             double xK, double exK, double a, double b,
+                                             double s2, double s4) {
+    const double v0 = is_call ? (S0 * (C.eb - exK) - K * (b - xK))
+                              : (K * (xK - a) - S0 * (exK - C.ea));
+    const double cst = is_call ? (C.c0 - K * C.c1) : C.c5;
+    return cst + C.w0 * v0 - exK * s2 + K * s4;
+}
+
+constexpr int kR = 4;   // options carried per lane in phase 2 (independent rotation chains)
+
+// Angle sums of up to kR options on lanes k = k1, k1 + G, ...:
+//   s2_j = sum_k T2_k cos(k th_j) + T3_k sin(k th_j),  s4_j = sum_k T4_k sin(k th_j)
+// the angle u_k (xK_j - a) advances by an e^{i G th_j} rotation, exact re-anchor every kAnchor
+// steps; one (T2, T3) ds_read_b128 + one T4 read serve all kR options.
+__device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double (&dx)[kR],
+                                             double ba, const double* tu, const double2* t23,
+                                             const double* t4, double (&s2)[kR],
+                                             double (&s4)[kR]) {
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+        s2[j] = 0.0;
+        s4[j] = 0.0;
+    }
+    if (k1 >= N) return;
+    double cx[kR], sx[kR], cs[kR], ss[kR];
+    const double ustep = G * dh::kPi / ba;
+    const double u1 = tu[k1];
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+        dh::dsincos(u1 * dx[j], &sx[j], &cx[j]);
+        dh::dsincos(ustep * dx[j], &ss[j], &cs[j]);
+    }
+    int n = 0;
+    for (int k = k1; k < N; k += G, ++n) {
+        if (n == kAnchor) {
+            const double uk = tu[k];
+#pragma unroll
+            for (int j = 0; j < kR; ++j) dh::dsincos(uk * dx[j], &sx[j], &cx[j]);
+            n = 0;
+        }
+        const double2 a23 = t23[k];
+        const double a4 = t4[k];
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+            s2[j] = fma(a23.x, cx[j], s2[j]);
+            s2[j] = fma(a23.y, sx[j], s2[j]);
+            s4[j] = fma(a4, sx[j], s4[j]);
+            const double cn = cx[j] * cs[j] - sx[j] * ss[j];
+            sx[j] = sx[j] * cs[j] + cx[j] * ss[j];
+            cx[j] = cn;
+        }
+    }
+}
+
+#ifndef DH_MIN_WAVES
+#define DH_MIN_WAVES 1     // occupancy hint (waves per SIMD) for the register allocator
+#endif
+
+template <int TPT>
+__global__ __launch_bounds__(kBlock, DH_MIN_WAVES) void cos_price_kernel(PriceArgs A) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int kTasks = kBlock / TPT;
     const int slot = threadIdx.x / TPT;
     const int t = threadIdx.x % TPT;
     const int N = A.N;
     const int64_t n_tasks = A.paired ? A.P : A.P * (int64_t)A.n_tiles;
-    const int64_t task = (int64_t)blockIdx.x * kTasks + slot;
+    // the task index is wave-uniform: make that visible so params live in SGPRs
+    const int64_t task = (int64_t)blockIdx.x * kTasks + __builtin_amdgcn_readfirstlane(slot);
     const bool active = task < n_tasks;
     const int64_t p = active ? (A.paired ? task : task / A.n_tiles) : 0;
     const int tile = active ? (A.paired ? 0 : (int)(task % A.n_tiles)) : 0;
+    DH_RSTAMP(A, 0);
+    DH_STAMP(A, 1);
 
-    double* tab = smem + (size_t)slot * (kTabFields * N + 2 * kTileMax);
-    double* tu = tab;
-    double* tw = tab + N;
-    double* tcb = tab + 2 * N;
-    double* tsb = tab + 3 * N;
-    double* ti1 = tab + 4 * N;
-    double* tiu = tab + 5 * N;
-    double* tprice = tab + kTabFields * N;       // [kTileMax] prices of this task (loss mode)
-    double* tflag = tprice + kTileMax;           // [kTileMax] 1.0 if invalid
+    // LDS per task: (T2,T3)[N] | u[N] | T4[N] | reduction | option data | loss | clamp list
+    double* base = smem + (size_t)slot * task_lds_doubles(N, TPT);
+    double2* t23 = (double2*)base;
+    double* tu = base + 2 * N;
+    double* t4 = base + 3 * N;
+    double* red = base + 4 * N;
+    double* lK = red + 4 * (TPT / 64);                 // [kTileMax] strikes
+    double* lmkt = lK + kTileMax;                      // [kTileMax] market prices
+    double* lsse = lmkt + kTileMax;                    // [kTileMax]
+    double* lbad = lsse + kTileMax;                    // [kTileMax]
+    int* lcall = (int*)(lbad + kTileMax);              // [kTileMax]
+    int* lperm = lcall + kTileMax;                     // [kTileMax]
+    int* lclamp = lperm + kTileMax;                    // [kTileMax] clamped option indices
+    int* ncl = lclamp + kTileMax;                      // [1]
+    int* nclmax = (int*)(smem + (size_t)kTasks * task_lds_doubles(N, TPT));   // [1] block max
 
     const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
     int opt0 = 0, nopt = 0;
@@ -113,154 +404,137 @@ __global__ __launch_bounds__(kBlock) void cos_price_kernel(PriceArgs A) {
             nopt = tl.y;
         }
     }
+    // prefetch this tile's option data (first chunk in registers across the truncation math)
+    const bool pf = active && t < nopt;
+    const double pK = pf ? A.K[opt0 + t] : 0.0;
+    const double pM = (pf && A.mkt) ? A.mkt[opt0 + t] : 0.0;
+    const int pC = pf ? A.call[opt0 + t] : 0;
+    const int pP = pf ? A.perm[opt0 + t] : 0;
+    if (t == 0) *ncl = 0;
+    if (threadIdx.x == 0) *nclmax = 0;
     const double T = active ? A.T[opt0] : 1.0;
     double a0, b0;
     dh::trunc_unclamped(P, T, A.L, a0, b0);
     const double ba0 = b0 - a0;
-    const double scale0 = 2.0 / ba0;
-
-    // ---- phase 1: COS table of this (p, T) ----
-    if (active) {
-        for (int k = t; k < N; k += TPT) {
-            const double u = k * dh::kPi / ba0;
-            const cplx phi = dh::cf_eval(P, u, T);
-            double sa, ca;
-            sincos(u * a0, &sa, &ca);
-            // Re(phi * exp(-i u a)) (double_heston.py:187); 2/(b-a) of V_k folded in; k=0 halved
-            double w = (phi.re * ca + phi.im * sa) * scale0;
-            double sb, cb;
-            sincos(u * ba0, &sb, &cb);
-            tu[k] = u;
-            tw[k] = (k == 0) ? 0.5 * w : w;
-            tcb[k] = cb;
-            tsb[k] = sb;
-            ti1[k] = 1.0 / (1.0 + u * u);
-            tiu[k] = 1.0 / u;
-        }
-    }
-    __syncthreads();
-
-    // ---- phase 2: per-option reductions ----
-    int G = 64;
-    if (active) {
-        const int want = TPT / max(nopt, 1);
-        G = 1;
-        while (G * 2 <= want && G < 64) G *= 2;
-        while (G > 1 && G / 2 >= N) G /= 2;  // no more lanes than terms
-    }
     const double disc = exp(-P.r * T);
-    const int opts_per_pass = TPT / G;
-    for (int base = 0; base < nopt; base += opts_per_pass) {
-        const int oi = base + t / G;
-        const int gl = t % G;
-        const bool valid = active && oi < nopt;
-        double acc = 0.0;
-        if (valid) {
-            const int m = opt0 + oi;
-            const double Kin = A.K[m];
-            const double K = (A.strike_mode == DH_STRIKE_PCT_SPOT) ? Kin * P.S0 / 100.0 : Kin;
-            const bool is_call = A.call[m] != 0;
-            const double xK = log(K / P.S0);
-            // Python min/max semantics (a NaN a0 stays NaN), double_heston.py:136-137
-            const double a = (xK - 0.1 < a0) ? xK - 0.1 : a0;
-            const double b = (xK + 0.1 > b0) ? xK + 0.1 : b0;
-            const double exK = exp(xK);
-            const double eb = exp(b), ea = exp(a);
-            const int per = (N + G - 1) / G;
-            const int k_lo = gl * per;
-            const int k_hi = min(N, k_lo + per);
-            if (a == a0 && b == b0) {
-                for (int k = k_lo; k < k_hi; ++k) {
-                    double v;
-                    if (k == 0) {
-                        // chi_0 = e^d - e^c, psi_0 = d - c
-                        v = is_call ? (P.S0 * (eb - exK) - K * (b - xK))
-                                    : (K * (xK - a) - P.S0 * (exK - ea));
-                    } else {
-                        const double u = tu[k];
-                        double sx, cx;
-                        sincos(u * (xK - a), &sx, &cx);
-                        v = payoff_coeff(is_call, u, ti1[k], tiu[k], tcb[k], tsb[k], cx, sx, eb,
-                                         ea, exK, P.S0, K);
-                    }
-                    acc += tw[k] * v;
-                }
-            } else {
-                // clamp-widened range: this option needs its own u grid and CF values
-                const double ba = b - a;
-                const double scale = 2.0 / ba;
-                for (int k = k_lo; k < k_hi; ++k) {
-                    const double u = k * dh::kPi / ba;
-                    const cplx phi = dh::cf_eval(P, u, T);
-                    double sa, ca;
-                    sincos(u * a, &sa, &ca);
-                    double w = (phi.re * ca + phi.im * sa) * scale;
-                    double v;
-                    if (k == 0) {
-                        w *= 0.5;
-                        v = is_call ? (P.S0 * (eb - exK) - K * (b - xK))
-                                    : (K * (xK - a) - P.S0 * (exK - ea));
-                    } else {
-                        double sb, cb, sx, cx;
-                        sincos(u * ba, &sb, &cb);
-                        sincos(u * (xK - a), &sx, &cx);
-                        v = payoff_coeff(is_call, u, 1.0 / (1.0 + u * u), 1.0 / u, cb, sb, cx, sx,
-                                         eb, ea, exK, P.S0, K);
-                    }
-                    acc += w * v;
-                }
-            }
-        }
-        // subgroup butterfly (G lanes, aligned inside one wave; all lanes of the wave take part)
-        for (int off = 1; off < G; off <<= 1) acc += __shfl_xor(acc, off, 64);
-        if (valid && gl == 0) {
-            const double price = disc * acc;  // e^{-rT} sum' (double_heston.py:190)
-            const int m = opt0 + oi;
-            if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
-            if (A.part_sse) {
-                const double mk = A.mkt[m];
-                const double rel = (price - mk) / mk;
-                tprice[oi] = rel * rel;
-                // lbfgs_calibrator.py:152: NaN, inf or <= 0 is invalid
-                tflag[oi] = (isnan(price) || isinf(price) || price <= 0.0) ? 1.0 : 0.0;
-            }
-        }
+    const bool pct = A.strike_mode == DH_STRIKE_PCT_SPOT;
+    if (pf) {
+        lK[t] = pct ? pK * P.S0 / 100.0 : pK;
+        lmkt[t] = pM;
+        lcall[t] = pC;
+        lperm[t] = pP;
     }
+    for (int i = t + TPT; active && i < nopt; i += TPT) {
+        const double Kin = A.K[opt0 + i];
+        lK[i] = pct ? Kin * P.S0 / 100.0 : Kin;
+        lmkt[i] = A.mkt ? A.mkt[opt0 + i] : 0.0;
+        lcall[i] = A.call[opt0 + i];
+        lperm[i] = A.perm[opt0 + i];
+    }
+    DH_STAMP(A, 2);
 
-    // ---- phase 3: fixed-order per-task loss partial ----
-    if (A.part_sse) {
-        __syncthreads();
-        if (active && t < 64) {
-            double s = 0.0, f = 0.0;
-            for (int i = t; i < nopt; i += 64) {
-                s += tprice[i];
-                f += tflag[i];
+    // One table-build site for both passes (a second inlined copy of the CF costs ~80 VGPRs):
+    //   it = 0   table of (p, T) on the un-clamped range, then every option of the tile;
+    //   it >= 1  table rebuilt on the widened range of the (it-1)-th clamped option
+    //            (double_heston.py:135-137), then that option alone.
+    // The trip count is block-uniform (max over the block's tasks) because of the barriers.
+    int n_iter = 1;
+    for (int it = 0; it < n_iter; ++it) {
+        bool work = active;
+        int oi1 = 0;
+        double a = a0, b = b0, K1 = P.S0, xK1 = 0.0;
+        if (it > 0) {
+            work = active && it - 1 < *ncl;
+            oi1 = work ? lclamp[it - 1] : 0;
+            K1 = work ? lK[oi1] : P.S0;
+            xK1 = log(K1 / P.S0);
+            a = (xK1 - 0.1 < a0) ? xK1 - 0.1 : a0;          // Python min/max (:136-137)
+            b = (xK1 + 0.1 > b0) ? xK1 + 0.1 : b0;
+            __syncthreads();                                  // previous table readers are done
+        }
+        // table build (its barrier also publishes the prefetched option data on it = 0)
+        const Consts C = build_table<TPT>(P, T, a, b, work, N, t, tu, t23, t4, red);
+        if (it == 0) {
+            DH_STAMP(A, 3);
+            // ---- phase 2: option groups of kR options on G lanes each ----
+            const int R = min(kR, max(nopt, 1));
+            const int ngroups = (nopt + R - 1) / R;
+            int G = 1;
+            while (G * 2 <= TPT / max(ngroups, 1) && G < 64) G *= 2;
+            while (G > 1 && G / 2 >= N - 1) G /= 2;           // no more lanes than terms k >= 1
+            const int groups_per_pass = TPT / G;
+            for (int pass = 0; pass < ngroups; pass += groups_per_pass) {
+                const int gi = pass + t / G;
+                const int gl = t % G;
+                const bool gvalid = active && gi < ngroups;
+                double dx[kR], xK[kR];
+                bool use[kR];
+#pragma unroll
+                for (int j = 0; j < kR; ++j) {
+                    const int oi = gi * R + j;
+                    use[j] = gvalid && j < R && oi < nopt;
+                    const double K = use[j] ? lK[oi] : P.S0;
+                    xK[j] = log(K / P.S0);
+                    if (use[j] && (xK[j] - 0.1 < a0 || xK[j] + 0.1 > b0)) {   // widened range
+                        if (gl == 0) lclamp[atomicAdd(ncl, 1)] = oi;
+                        use[j] = false;
+                    }
+                    dx[j] = use[j] ? xK[j] - a0 : 0.0;
+                }
+                double s2[kR], s4[kR];
+                angle_sums_r(1 + gl, G, N, dx, ba0, tu, t23, t4, s2, s4);
+                for (int off = 1; off < G; off <<= 1) {
+#pragma unroll
+                    for (int j = 0; j < kR; ++j) {
+                        s2[j] += __shfl_xor(s2[j], off, 64);
+                        s4[j] += __shfl_xor(s4[j], off, 64);
+                    }
+                }
+                if (gl == 0) {
+#pragma unroll
+                    for (int j = 0; j < kR; ++j) {
+                        if (!use[j]) continue;
+                        const int oi = gi * R + j;
+                        const double sum = option_sum(C, lcall[oi] != 0, P.S0, lK[oi], xK[j],
+                                                      exp(xK[j]), a0, b0, s2[j], s4[j]);
+                        record_price(A, p, lperm[oi], lmkt[oi], oi, disc * sum, lsse, lbad);
+                    }
+                }
+            }
+            __syncthreads();
+            DH_STAMP(A, 4);
+            if (t == 0 && active) atomicMax(nclmax, *ncl);
+            __syncthreads();
+            n_iter = 1 + *nclmax;
+        } else {
+            double dx[kR] = {work ? xK1 - a : 0.0, 0.0, 0.0, 0.0};
+            double s2[kR], s4[kR];
+            if (work && t < 64) {
+                angle_sums_r(1 + t, 64, N, dx, b - a, tu, t23, t4, s2, s4);
+            } else {
+                s2[0] = 0.0;
+                s4[0] = 0.0;
             }
             for (int off = 1; off < 64; off <<= 1) {
-                s += __shfl_xor(s, off, 64);
-                f += __shfl_xor(f, off, 64);
+                s2[0] += __shfl_xor(s2[0], off, 64);
+                s4[0] += __shfl_xor(s4[0], off, 64);
             }
-            if (t == 0) {
-                A.part_sse[task] = s;
-                A.part_bad[task] = (int)f;
+            if (work && t == 0) {
+                const double sum = option_sum(C, lcall[oi1] != 0, P.S0, K1, xK1, exp(xK1), a, b,
+                                              s2[0], s4[0]);
+                record_price(A, p, lperm[oi1], lmkt[oi1], oi1, disc * sum, lsse, lbad);
             }
         }
     }
-}
 
-__global__ void loss_finalize_kernel(const double* __restrict__ part_sse,
-                                     const int* __restrict__ part_bad, int n_tiles, int S,
-                                     double* __restrict__ sse, int32_t* __restrict__ n_bad) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
-    double acc = 0.0;
-    int bad = 0;
-    for (int j = 0; j < n_tiles; ++j) {
-        acc += part_sse[(int64_t)s * n_tiles + j];
-        bad += part_bad[(int64_t)s * n_tiles + j];
+    // ---- phase 3: fixed-order per-task loss partial, last arriver finalises the param set ----
+    DH_STAMP(A, 5);
+    if (A.part_sse) {
+        __syncthreads();
+        if (active && t < 64) task_loss(A, p, task, nopt, t, lsse, lbad);
     }
-    sse[s] = acc;
-    n_bad[s] = bad;
+    DH_STAMP(A, 6);
+    DH_RSTAMP(A, 7);
 }
 
 __global__ void cf_kernel(const double* __restrict__ prm, const double* __restrict__ u, int n,
@@ -335,7 +609,7 @@ struct DevBuf {
 
 size_t lds_bytes(int N, int tpt) {
     const int tasks = kBlock / tpt;
-    return (size_t)tasks * (kTabFields * (size_t)N + 2 * kTileMax) * sizeof(double);
+    return ((size_t)tasks * task_lds_doubles(N, tpt) + 2) * sizeof(double);
 }
 
 int pick_tpt(int N) { return N >= 256 ? 256 : (N >= 128 ? 128 : 64); }
@@ -345,8 +619,13 @@ int pick_tpt(int N) { return N >= 256 ? 256 : (N >= 128 ? 128 : 64); }
 struct dh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf params, out, sse, bad, part_sse, part_bad, aux0, aux1, aux2, aux3;
+    DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, aux0, aux1, aux2,
+        aux3;
     bool attr_set = false;
+    int exact = 0;          // validation mode: every option through the per-term exact path
+    int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
+    DevBuf stamps;
+    int64_t stamps_n = 0;
 };
 
 struct dh_surface {
@@ -390,12 +669,44 @@ int check_N(int N) {
     return DH_OK;
 }
 
+int launch_exact(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
+    const int64_t n_items = A.paired ? A.P : A.P * (int64_t)A.M;
+    double* prices = nullptr;
+    if (A.part_sse) {
+        HIP_TRY(ctx->exact_prices.reserve((size_t)n_items * 8));
+        prices = (double*)ctx->exact_prices.ptr;
+    }
+    const int64_t blocks = (n_items * 64 + kBlock - 1) / kBlock;
+    if (blocks > 0x7fffffffLL) return fail(DH_E_ARG, "too many items for one launch");
+    hipLaunchKernelGGL(cos_exact_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, A, A.M,
+                       prices);
+    HIP_TRY(hipGetLastError());
+    if (A.part_sse) {
+        const int S = (int)A.P;
+        hipLaunchKernelGGL(loss_from_prices_kernel, dim3((S * 64 + kBlock - 1) / kBlock),
+                           dim3(kBlock), 0, st, (const double*)prices, A.mkt, A.M, S, A.sse,
+                           A.n_bad);
+        HIP_TRY(hipGetLastError());
+    }
+    return DH_OK;
+}
+
 int launch_price(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
+    const int64_t n_tasks = A.paired ? A.P : A.P * (int64_t)A.n_tiles;
+    if (n_tasks == 0) return DH_OK;
+    if (A.exact) return launch_exact(ctx, A, st);
+    PriceArgs B = A;
+    if (ctx->stamps_on) {
+        const int tpb = kBlock / pick_tpt(A.N);
+        const int64_t nb = (n_tasks + tpb - 1) / tpb;
+        HIP_TRY(ctx->stamps.reserve((size_t)nb * kStamps * 8));
+        HIP_TRY(hipMemsetAsync(ctx->stamps.ptr, 0, (size_t)nb * kStamps * 8, st));
+        B.stamps = (unsigned long long*)ctx->stamps.ptr;
+        ctx->stamps_n = nb * kStamps;
+    }
     int rc = ensure_attrs(ctx);
     if (rc) return rc;
     const int tpt = pick_tpt(A.N);
-    const int64_t n_tasks = A.paired ? A.P : A.P * (int64_t)A.n_tiles;
-    if (n_tasks == 0) return DH_OK;
     const int tasks_per_block = kBlock / tpt;
     const int64_t blocks = (n_tasks + tasks_per_block - 1) / tasks_per_block;
     if (blocks > 0x7fffffffLL) return fail(DH_E_ARG, "too many tasks for one launch");
@@ -403,9 +714,9 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
     if (lds > 160 * 1024) return fail(DH_E_ARG, "COS table does not fit in LDS");
     dim3 grid((unsigned)blocks), block(kBlock);
     switch (tpt) {
-        case 64: hipLaunchKernelGGL(cos_price_kernel<64>, grid, block, lds, st, A); break;
-        case 128: hipLaunchKernelGGL(cos_price_kernel<128>, grid, block, lds, st, A); break;
-        default: hipLaunchKernelGGL(cos_price_kernel<256>, grid, block, lds, st, A); break;
+        case 64: hipLaunchKernelGGL(cos_price_kernel<64>, grid, block, lds, st, B); break;
+        case 128: hipLaunchKernelGGL(cos_price_kernel<128>, grid, block, lds, st, B); break;
+        default: hipLaunchKernelGGL(cos_price_kernel<256>, grid, block, lds, st, B); break;
     }
     HIP_TRY(hipGetLastError());
     return DH_OK;
@@ -462,7 +773,8 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->params, &ctx->out, &ctx->sse, &ctx->bad, &ctx->part_sse,
-                      &ctx->part_bad, &ctx->aux0, &ctx->aux1, &ctx->aux2, &ctx->aux3})
+                      &ctx->part_bad, &ctx->counter, &ctx->exact_prices, &ctx->stamps, &ctx->aux0,
+                      &ctx->aux1, &ctx->aux2, &ctx->aux3})
         b->release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -477,6 +789,35 @@ int dh_ctx_synchronize(dh_ctx* ctx) {
 }
 
 void* dh_ctx_stream(dh_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int dh_ctx_debug_stamps(dh_ctx* ctx, int on) {
+    if (!ctx) return fail(DH_E_ARG, "ctx is null");
+#ifdef DH_STAMPS
+    ctx->stamps_on = on ? 1 : 0;
+    return DH_OK;
+#else
+    (void)on;
+    return fail(DH_E_ARG, "library built without DH_STAMPS (use `make stamps`)");
+#endif
+}
+
+int dh_ctx_read_stamps(dh_ctx* ctx, unsigned long long* out, int64_t cap, int64_t* n) {
+    if (!ctx || !n) return fail(DH_E_ARG, "null argument");
+    *n = ctx->stamps_n;
+    if (!out || ctx->stamps_n == 0) return DH_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, ctx->stamps.ptr, (size_t)std::min<int64_t>(cap, ctx->stamps_n) * 8,
+                      hipMemcpyDeviceToHost));
+    return DH_OK;
+}
+
+int dh_ctx_set_exact(dh_ctx* ctx, int on) {
+    if (!ctx) return fail(DH_E_ARG, "ctx is null");
+    ctx->exact = on ? 1 : 0;
+    return DH_OK;
+}
 
 int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_t* is_call,
                       const double* mkt, int M, int strike_mode, dh_surface** out) {
@@ -572,6 +913,7 @@ static PriceArgs surface_args(const dh_surface* s, const double* d_params, int64
     A.perm = s->perm;
     A.tiles = s->tiles;
     A.n_tiles = s->n_tiles;
+    A.M = s->M;
     A.paired = 0;
     A.strike_mode = s->strike_mode;
     A.N = N;
@@ -590,6 +932,7 @@ int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_param
     rc = set_device(ctx);
     if (rc) return rc;
     PriceArgs A = surface_args(s, d_params, P, N, L);
+    A.exact = ctx->exact;
     A.out = d_out;
     return launch_price(ctx, A, stream ? (hipStream_t)stream : ctx->stream);
 }
@@ -615,34 +958,20 @@ int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params
     const size_t nparts = (size_t)S * s->n_tiles;
     HIP_TRY(ctx->part_sse.reserve(nparts * 8));
     HIP_TRY(ctx->part_bad.reserve(nparts * 4));
+    const size_t cap0 = ctx->counter.cap;
+    HIP_TRY(ctx->counter.reserve((size_t)S * 4));
+    if (ctx->counter.cap != cap0) {       // fresh counters start at zero; kernels self-reset
+        HIP_TRY(hipMemsetAsync(ctx->counter.ptr, 0, ctx->counter.cap, st));
+    }
     PriceArgs A = surface_args(s, d_params, S, N, L);
+    A.exact = ctx->exact;
     A.out = d_prices;
     A.part_sse = (double*)ctx->part_sse.ptr;
     A.part_bad = (int*)ctx->part_bad.ptr;
-    rc = launch_price(ctx, A, st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(loss_finalize_kernel, dim3((S + 63) / 64), dim3(64), 0, st, A.part_sse,
-                       A.part_bad, s->n_tiles, S, d_sse, d_n_bad);
-    HIP_TRY(hipGetLastError());
-    return DH_OK;
-}
-
-int dh_surface_partials_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S,
-                            int N, double L, double* d_part_sse, int32_t* d_part_bad,
-                            void* stream) {
-    if (!ctx || !s || (S > 0 && (!d_params || !d_part_sse || !d_part_bad)))
-        return fail(DH_E_ARG, "null argument");
-    if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
-    int rc = check_N(N);
-    if (rc) return rc;
-    if (S < 0) return fail(DH_E_ARG, "S < 0");
-    if (S == 0 || s->M == 0) return DH_OK;
-    rc = set_device(ctx);
-    if (rc) return rc;
-    PriceArgs A = surface_args(s, d_params, S, N, L);
-    A.part_sse = d_part_sse;
-    A.part_bad = (int*)d_part_bad;
-    return launch_price(ctx, A, stream ? (hipStream_t)stream : ctx->stream);
+    A.counter = (unsigned*)ctx->counter.ptr;
+    A.sse = d_sse;
+    A.n_bad = (int*)d_n_bad;
+    return launch_price(ctx, A, st);
 }
 
 int dh_surface_price(dh_ctx* ctx, const dh_surface* s, const double* params, int64_t P, int N,
@@ -730,6 +1059,8 @@ int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const dou
     A.call = (const int8_t*)ctx->aux2.ptr;
     A.perm = (const int*)ctx->aux3.ptr;
     A.paired = 1;
+    A.M = (int)P;
+    A.exact = ctx->exact;
     A.strike_mode = DH_STRIKE_ABSOLUTE;
     A.N = N;
     A.L = L;

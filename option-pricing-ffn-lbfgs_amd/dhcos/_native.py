@@ -39,6 +39,10 @@ SIGNATURES = {
     "dh_ctx_destroy": (C.c_int, [_vp]),
     "dh_ctx_synchronize": (C.c_int, [_vp]),
     "dh_ctx_stream": (_vp, [_vp]),
+    "dh_ctx_set_exact": (C.c_int, [_vp, C.c_int]),
+    "dh_ctx_debug_stamps": (C.c_int, [_vp, C.c_int]),
+    "dh_ctx_read_stamps": (C.c_int, [_vp, C.POINTER(C.c_ulonglong), C.c_int64,
+                                     C.POINTER(C.c_int64)]),
     "dh_surface_create": (C.c_int, [_vp, _dp, _dp, _i8p, _dp, C.c_int, C.c_int, C.POINTER(_vp)]),
     "dh_surface_destroy": (C.c_int, [_vp]),
     "dh_surface_size": (C.c_int, [_vp, _i32p, _i32p]),
@@ -47,8 +51,6 @@ SIGNATURES = {
     "dh_surface_price_dev": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp, _vp]),
     "dh_surface_loss_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp,
                                       _vp]),
-    "dh_surface_partials_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp,
-                                          _vp]),
     "dh_price_pairs": (C.c_int, [_vp, _dp, _dp, _dp, _i8p, C.c_int64, C.c_int, C.c_double, _dp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
@@ -133,6 +135,23 @@ class Context:
     @property
     def stream(self) -> int:
         return load().dh_ctx_stream(self._h) or 0
+
+    def set_exact(self, on: bool):
+        """Validation mode: price every option by the per-term reference-order path."""
+        _check(load().dh_ctx_set_exact(self._h, 1 if on else 0))
+
+    def debug_stamps(self, on: bool):
+        """Diagnostic build only: record per-block phase stamps of the next COS launches."""
+        _check(load().dh_ctx_debug_stamps(self._h, 1 if on else 0))
+
+    def read_stamps(self):
+        n = C.c_int64(0)
+        _check(load().dh_ctx_read_stamps(self._h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        if n.value:
+            _check(load().dh_ctx_read_stamps(self._h, out.ctypes.data_as(C.POINTER(C.c_ulonglong)),
+                                             n.value, C.byref(n)))
+        return out.reshape(-1, 8)
 
     def synchronize(self):
         _check(load().dh_ctx_synchronize(self._h))
@@ -256,12 +275,6 @@ class Surface:
                                           float(L), _vp(d_sse), _vp(d_bad),
                                           _vp(d_prices) if d_prices else None,
                                           _vp(stream) if stream else None))
-
-    def partials_dev(self, d_params: int, S: int, d_part_sse: int, d_part_bad: int, N=128,
-                     L=10.0, stream: int = 0):
-        _check(load().dh_surface_partials_dev(self.ctx.handle, self._h, _vp(d_params), int(S),
-                                              int(N), float(L), _vp(d_part_sse), _vp(d_part_bad),
-                                              _vp(stream) if stream else None))
 
 
 _tls = threading.local()
