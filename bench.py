@@ -38,11 +38,12 @@ from dhcos import _native                                      # noqa: E402
 from dhcos.calibrator import (DoubleHestonJumpCalibrator,      # noqa: E402
                               fd_request_points, x_to_model)
 
-# algorithmic work of the implemented algorithm, fp64 flop-equivalents (DESIGN.md "Roofline"):
-# add/mul = 1, fma = 2, exp/log/sin/cos/atan2 = 20, div/sqrt/hypot = 8 (SURVEY 8(d) weights)
-FLOP_TAB = 940         # per COS-table entry (p, T, k): CF (815) + phase, cos/sin(u(b-a)), T2..T4
+# Algorithmic work of the implemented algorithm in fp64 flop-equivalents (DESIGN.md "Roofline"),
+# frozen: add/mul = 1, fma = 2, and each elementary function = 2 x its gfx950 ocml instruction
+# count (exp 42, log 98, sin+cos 148, atan2 105, sqrt 22, div/rcp 12 instructions).
+FLOP_TAB = 3137        # per COS-table entry (p, T, k): fast-form CF + phase + T2..T4 + k-sums
 FLOP_TERM = 12         # per (param set, option, k >= 1): 3 fma + 1 complex rotation
-FLOP_OPT = 120         # per (param set, option): log(K/S0), exp, k = 0 term, constants
+FLOP_OPT = 596         # per (param set, option): log, exp, step rotation, k = 0 term, loss
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector peak (spec)
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BYTES_PER_OPTION = 8 + 8 + 1 + 8 + 4   # K, T, is_call, mkt, perm read per (param set, option)
@@ -191,7 +192,7 @@ def main():
     prices_per_step = S * M
     value = prices_per_step * K_ * world / dt
 
-    # ---- roofline of the dominant kernel (cos_price_kernel, loss mode; one launch per step) ----
+    # ---- roofline of the dominant op: one request = cos_table_kernel + cos_option_kernel ----
     reps = max(20, min(K_, 200))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(reps)]
@@ -210,7 +211,7 @@ def main():
     roofline = {"bound": "valu_fp64", "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4),
                 "traffic": pmc_traffic(args.config),
-                "kernel": "cos_price_kernel<%d>" % (256 if N >= 256 else (128 if N >= 128 else 64)),
+                "kernel": "cos_table_kernel + cos_option_kernel (one request, HIP events)",
                 "kernel_ms": round(ker_ms, 5), "flop_per_launch": flop,
                 "alg_bytes_per_launch": alg_bytes,
                 "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),

@@ -57,6 +57,10 @@ __device__ __forceinline__ cplx csqrt_p(cplx z) {
 // ~2 ulp for |x| < 2^20 (every argument on this path is bounded by N pi plus the CF phases);
 // accuracy degrades gracefully beyond, and non-finite x gives NaN like libm.  Replaces ocml's
 // sincos, whose inlined Payne-Hanek branch costs ~100 VGPRs per call site.
+__device__ __forceinline__ double flip_sign(double v, int neg) {   // neg: 0 or 1
+    return __hiloint2double(__double2hiint(v) ^ (neg << 31), __double2loint(v));
+}
+
 __device__ __forceinline__ void dsincos(double x, double* sp, double* cp) {
     const double q = rint(x * 6.36619772367581382433e-01);           // x * 2/pi
     double r = fma(-q, 1.57079632679489655800e+00, x);                 // pi/2, 3 parts
@@ -74,11 +78,11 @@ __device__ __forceinline__ void dsincos(double x, double* sp, double* cp) {
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double c = w + (((1.0 - w) - hz) + z * pc);
-    const double qm = q - 4.0 * floor(q * 0.25);                       // quadrant in {0,1,2,3}
-    const bool swap = (qm == 1.0) || (qm == 3.0);
-    const double s1 = swap ? c : s, c1 = swap ? s : c;
-    *sp = (qm >= 2.0) ? -s1 : s1;
-    *cp = (qm == 1.0 || qm == 2.0) ? -c1 : c1;
+    // quadrant from the low bits of q (q is an exact integer; |q| < 2^31 on this path)
+    const int qi = (int)q;
+    const bool swap = qi & 1;
+    *sp = flip_sign(swap ? c : s, (qi >> 1) & 1);
+    *cp = flip_sign(swap ? s : c, ((qi + 1) >> 1) & 1);
 }
 
 __device__ __forceinline__ cplx cexp_(cplx z) {
@@ -91,11 +95,41 @@ __device__ __forceinline__ cplx cexp_(cplx z) {
 // Principal log: arg in (-pi, pi].
 __device__ __forceinline__ cplx clog_(cplx z) { return {log(hypot(z.re, z.im)), atan2(z.im, z.re)}; }
 
-// ---- lean fp64 elementary functions for the hot kernel (fdlibm algorithms, < 1-2 ulp) -------
-// ocml's fp64 log / atan2 cost ~90-100 VALU instructions each (double-double internals); these
-// restate fdlibm's e_log.c / s_atan.c / e_atan2.c with select-based interval reduction.
+// ---- lean fp64 elementary functions for the hot kernels ------------------------------------
+// Measured on gfx950 (tools/ubench/fp64_latency.hip, cycles of issue per wave64): IEEE division
+// ~70, ocml sqrt ~110, exp ~120, ocml log ~456, ocml atan2 ~255, an fp64 FMA ~5.5.  The COS
+// table is issue-bound, so these restate the needed functions with v_rcp_f64 / v_rsq_f64 seeds
+// and Newton/Goldschmidt steps (<= ~2 ulp; NaN in gives NaN out; used on finite operands).
 
-// log(x) for any x: x = 2^k (1 + f), sqrt(1/2) <= 1 + f < sqrt(2), s = f / (2 + f).
+// 1/x: v_rcp_f64 seed + two Newton steps.
+__device__ __forceinline__ double drcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
+// sqrt(x) and 1/sqrt(x) together: v_rsq_f64 seed + one Goldschmidt step + residual correction.
+__device__ __forceinline__ void dsqrt_rsqrt(double x, double& sq, double& rs) {
+    const double y0 = __builtin_amdgcn_rsq(x);
+    double g = x * y0, h = 0.5 * y0;
+    const double r = fma(-g, h, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    const double d = fma(-g, g, x);
+    sq = fma(h, d, g);
+    rs = 2.0 * h;
+    if (x == 0.0 || isinf(x)) sq = x;
+}
+
+__device__ __forceinline__ double dsqrt(double x) {
+    double s, r;
+    dsqrt_rsqrt(x, s, r);
+    return s;
+}
+
+// log(x): fdlibm e_log.c, x = 2^k (1 + f), sqrt(1/2) <= 1 + f < sqrt(2), s = f / (2 + f).
 __device__ __forceinline__ double dlog(double x) {
     int k;
     double m = frexp(x, &k);                         // m in [0.5, 1)
@@ -103,7 +137,7 @@ __device__ __forceinline__ double dlog(double x) {
     m = lo ? 2.0 * m : m;
     k = lo ? k - 1 : k;
     const double f = m - 1.0;
-    const double s = f / (2.0 + f);
+    const double s = f * drcp(2.0 + f);
     const double z = s * s, w = z * z;
     const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 +
                       w * 1.531383769920937332e-01));
@@ -119,49 +153,35 @@ __device__ __forceinline__ double dlog(double x) {
     return r;
 }
 
-// atan(t) for t >= 0 (fdlibm s_atan.c), interval reduction by selects and one division.
-__device__ __forceinline__ double datan_pos(double t) {
-    // id: -1 (t < 0.4375), 0 (< 0.6875), 1 (< 1.1875), 2 (< 2.4375), 3 (otherwise)
-    const bool r0 = t >= 0.4375, r1 = t >= 0.6875, r2 = t >= 1.1875, r3 = t >= 2.4375;
-    // t' = (a t + b) / (c t + d)
-    const double a = r3 ? 0.0 : (r2 ? 1.0 : (r1 ? 1.0 : (r0 ? 2.0 : 1.0)));
-    const double b = r3 ? -1.0 : (r2 ? -1.5 : (r1 ? -1.0 : (r0 ? -1.0 : 0.0)));
-    const double c = r3 ? 1.0 : (r2 ? 1.5 : (r1 ? 1.0 : (r0 ? 1.0 : 0.0)));
-    const double d = r3 ? 0.0 : (r2 ? 1.0 : (r1 ? 1.0 : (r0 ? 2.0 : 1.0)));
-    const double x = fma(a, t, b) / fma(c, t, d);
-    const double hi = r3 ? 1.57079632679489655800e+00 : (r2 ? 9.82793723247329054082e-01 :
-                      (r1 ? 7.85398163397448278999e-01 : 4.63647609000806093515e-01));
-    const double lo = r3 ? 6.12323399573676588613e-17 : (r2 ? 1.39033110312309984516e-17 :
-                      (r1 ? 3.06161699786838301793e-17 : 2.26987774529616870924e-17));
-    const double z = x * x, w = z * z;
+// atan2(y, x) in (-pi, pi]: t = min/max in [0, 1]; for t > tan(pi/8) use
+// atan t = pi/4 + atan((t - 1)/(t + 1)); the fdlibm s_atan.c polynomial on |t'| <= tan(pi/8).
+__device__ __forceinline__ double datan2(double y, double x) {
+    const double ax = fabs(x), ay = fabs(y);
+    const double mx = fmax(ax, ay), mn = fmin(ax, ay);
+    const double t = mn * drcp(mx);
+    const bool big = t > 0.41421356237309503;
+    const double tr = big ? (t - 1.0) * drcp(t + 1.0) : t;
+    const double z = tr * tr, w = z * z;
     const double s1 = z * (3.33333333333329318027e-01 + w * (1.42857142725034663711e-01 +
                       w * (9.09088713343650656196e-02 + w * (6.66107313738753120669e-02 +
                       w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
     const double s2 = w * (-1.99999999998764832476e-01 + w * (-1.11111104054623557880e-01 +
                       w * (-7.69187620504482999495e-02 + w * (-5.83357013379057348645e-02 +
                       w * -3.65315727442169155270e-02))));
-    const double small = x - x * (s1 + s2);
-    const double big = hi - ((x * (s1 + s2) - lo) - x);
-    return r0 ? big : small;
+    const double at = tr - tr * (s1 + s2);
+    double a = big ? 7.85398163397448278999e-01 + (at + 3.06161699786838301793e-17) : at;
+    a = (ay > ax) ? (1.57079632679489655800e+00 - a) + 6.12323399573676588613e-17 : a;
+    a = (x < 0.0 || (x == 0.0 && signbit(x) && ay == 0.0))
+            ? (3.14159265358979311600e+00 - a) + 1.22464679914735317720e-16 : a;
+    a = (mx == 0.0 && !(x < 0.0 || signbit(x))) ? 0.0 : a;            // atan2(+-0, +0)
+    a = copysign(a, y);
+    return (isnan(x) || isnan(y)) ? x + y : a;
 }
 
-// atan2(y, x), principal value in (-pi, pi] (fdlibm e_atan2.c quadrant logic) for finite x, y.
-__device__ __forceinline__ double datan2(double y, double x) {
-    const double ax = fabs(x), ay = fabs(y);
-    const double z = datan_pos(ay / ax);             // y/x = +-inf and 0/0 handled below
-    const double pi = 3.1415926535897931160e+00, pi_lo = 1.2246467991473531772e-16;
-    double r = (x >= 0.0) ? z : pi - (z - pi_lo);
-    r = (ay == 0.0 && x >= 0.0) ? 0.0 : r;            // atan2(+-0, x >= 0) = +-0
-    r = (ay == 0.0 && x < 0.0) ? pi : r;              // atan2(+-0, x < 0) = +-pi
-    r = (ax == 0.0 && ay != 0.0) ? 1.57079632679489655800e+00 : r;
-    r = copysign(r, y);
-    return (isnan(x) || isnan(y)) ? x + y : r;
-}
-
-// z1 / z2 through one fp64 reciprocal of |z2|^2 (no Smith scaling: |z2| on this path stays far
+// z1 / z2 through one reciprocal of |z2|^2 (no Smith scaling: |z2| on this path stays far
 // from the fp64 over/underflow thresholds).
 __device__ __forceinline__ cplx cdiv_rcp(cplx a, cplx b) {
-    const double inv = 1.0 / fma(b.re, b.re, b.im * b.im);
+    const double inv = drcp(fma(b.re, b.re, b.im * b.im));
     return {(a.re * b.re + a.im * b.im) * inv, (a.im * b.re - a.re * b.im) * inv};
 }
 
@@ -242,17 +262,13 @@ __device__ __forceinline__ void factor_exponent(const FactorC& F, double u, doub
     const double s2u = F.s2 * u;
     const cplx dd = {fma(beta.re, beta.re, -beta.im * beta.im) + s2u * u,
                      2.0 * beta.re * beta.im + s2u};
-    // principal sqrt
-    const double h = sqrt(fma(dd.re, dd.re, dd.im * dd.im));
-    double dre, dim;
-    if (dd.re > 0.0) {
-        dre = sqrt(0.5 * (h + dd.re));
-        dim = 0.5 * dd.im / dre;
-    } else {
-        const double t = sqrt(0.5 * (h - dd.re));
-        dre = fabs(0.5 * dd.im / t);
-        dim = copysign(t, dd.im);
-    }
+    // principal sqrt: |dd|, then sqrt((|dd| + |Re|)/2) and its reciprocal (no division)
+    const double h = dsqrt(fma(dd.re, dd.re, dd.im * dd.im));
+    double sq, rs;
+    dsqrt_rsqrt(0.5 * (h + fabs(dd.re)), sq, rs);
+    const double other = 0.5 * dd.im * rs;
+    const double dre = dd.re > 0.0 ? sq : fabs(other);
+    const double dim = dd.re > 0.0 ? other : copysign(sq, dd.im);
     const cplx bm = {beta.re - dre, beta.im - dim};
     const cplx bp = {beta.re + dre, beta.im + dim};
     double es, ec;

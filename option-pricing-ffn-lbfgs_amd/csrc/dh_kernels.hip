@@ -1,24 +1,29 @@
-// dh_kernels.hip -- gfx950 kernels of the COS pricing / calibration-objective hot path.
+// dh_kernels.hip -- gfx950 kernels and C-ABI of the COS pricing / calibration-objective hot path.
 //
-// Work decomposition (DESIGN.md "Kernels"):
-//   task  = (param set p, tile); a tile is <= 256 options sharing one maturity T.
-//   block = 256 threads = 256/TPT tasks of TPT threads (TPT in {64,128,256}, chosen from N).
-//   phase 1  (CF table, once per (p, T)): the task's threads evaluate phi(u_k) for k < N and
-//            fold it with the k-only parts of the payoff coefficients (double_heston.py:141-158,
-//            176-190) into three LDS columns T2/T3/T4 plus three k-sums (call / put constants).
-//   phase 2  (per option): the COS sum splits into option-independent constants and two
-//            angle sums  S2 = sum_k T2_k cos(k th) + T3_k sin(k th),  S4 = sum_k T4_k sin(k th),
-//            th = pi (log(K/S0) - a) / (b - a).  A G-lane subgroup walks k interleaved (lane j:
-//            k = 1 + j, 1 + j + G, ...), advancing the angle by a complex rotation e^{i G th}
-//            with an exact sincos re-anchor every 64 steps, then reduces with DPP butterflies.
-//            Options whose [a, b] is widened by the log-strike clamp (double_heston.py:135-137)
-//            are queued and priced after a rebuild of the table on their own range (same code,
-//            block-uniform trip count).  Validation ("exact") mode instead runs cos_exact_kernel:
-//            per-term CF + sincos in the reference's operation order, one wave per option.
-//   phase 3  (loss mode): per-task fixed-order partial of sum rel^2 and #invalid; the last task
-//            of a param set to finish (agent-scope counter, release/acquire) sums the partials
-//            in tile order.  One launch per request, no float atomics, bitwise reproducible and
-//            independent of how many param sets share the launch.
+// Two kernels per request (DESIGN.md "Kernels"), each with its own small register footprint:
+//
+//   cos_table_kernel<TPT>  one table per (param set p, maturity group g):  for k < N
+//       w_k = Re(phi(u_k) e^{-i u_k a}) 2/(b-a)            (double_heston.py:48-97,163-168,187)
+//     (8 bytes per term) plus per-(p, g) constants c0/c1 (call), c5 (put), w0 (k = 0 weight),
+//     a, b, e^b, e^a reduced in a fixed order.  CF-bound; the table lands in an L2/MALL-resident
+//     workspace.
+//
+//   cos_option_kernel<TPT> one task per (p, tile), a tile = <= 256 options of one maturity:
+//     stage the (p, g) table into LDS, expanded to the strike-independent parts of chi_k/psi_k
+//     (k >= 1, double_heston.py:141-158):  u_k = k pi/(b-a),  T2_k = w_k S0/(1+u_k^2),
+//     T3_k = T2_k u_k,  T4_k = w_k/u_k;  per option only two angle sums remain
+//       S2 = sum_k T2_k cos(k th) + T3_k sin(k th),   S4 = sum_k T4_k sin(k th),
+//       th = pi (log(K/S0) - a)/(b - a),   price = e^{-rT} (const + w0 V_0 - e^{xK} S2 + K S4)
+//     computed by G lanes per group of kR options (lane j: k = 1 + j, 1 + j + G, ...), the
+//     angle advanced by complex rotations e^{i G th} with an exact sincos re-anchor every
+//     kAnchor steps, then DPP butterflies.  Options whose [a, b] is widened by the log-strike
+//     clamp (double_heston.py:135-137) are priced inline by a per-term path on their own range.
+//     Loss mode: fixed-order per-task partial of sum rel^2 and #invalid; the last task of p to
+//     finish (agent-scope counter, sc1 hand-off) sums the partials in tile order.  No float
+//     atomics: bitwise reproducible, independent of how many param sets share the launch.
+//
+//   Validation ("exact") mode runs cos_exact_kernel instead: per-term CF + sincos in the
+//   reference's operation order, one wave per option.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,17 +44,25 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kTileMax = 256;
 constexpr int kAnchor = 64;       // exact sincos re-anchor period of the angle recurrence
+constexpr int kR = 4;             // options carried per lane in the option kernel
+constexpr int kConsts = 8;        // c0, c1, c5, w0, a, b, e^b, e^a per table
+constexpr size_t kTableBudget = size_t(256) << 20;   // table workspace per chunk (MALL-sized)
+constexpr int kLdsMax = 160 * 1024;
 
 struct PriceArgs {
     const double* prm;      // [P][16]
-    int64_t P;
+    int64_t P;              // param sets of the whole request
+    int64_t p0, np;         // this launch covers param sets p0 .. p0 + np - 1
     const double* K;        // [M] sorted by T (absolute strike or K_relative)
     const double* T;        // [M]
     const int8_t* call;     // [M]
     const double* mkt;      // [M] or null
     const int* perm;        // [M] sorted -> caller index
     const int2* tiles;      // [n_tiles] (opt0, nopt)
-    int n_tiles;
+    const int* tile_group;  // [n_tiles] maturity group of each tile
+    const double* group_T;  // [n_groups]
+    int n_tiles, n_groups;
+    int opt_cap;            // >= largest tile (LDS option arrays)
     int paired;             // option i under param set i, one option per task
     int strike_mode;
     int exact;              // validation mode (host routes to cos_exact_kernel)
@@ -63,11 +76,13 @@ struct PriceArgs {
     unsigned* counter;      // [P] arrival counters (zero between launches)
     double* sse;            // [P] final sums (loss mode)
     int* n_bad;             // [P]
+    double* table;          // workspace: [np*tabs_per_p][N] = w_k
+    double* consts;         // workspace: [np*tabs_per_p][kConsts]
     unsigned long long* stamps;   // diagnostic builds (DH_STAMPS) only: [blocks][kStamps]
 };
 
 // In-kernel phase stamps, compiled only into the diagnostic build (make stamps): lane 0 of each
-// block writes s_memtime at the phase boundaries and s_memrealtime at start/end.
+// block of the option kernel writes s_memtime at its phase boundaries.
 constexpr int kStamps = 8;
 #ifdef DH_STAMPS
 #define DH_STAMP(A, i)                                                                     \
@@ -78,20 +93,204 @@ constexpr int kStamps = 8;
             (A).stamps[(size_t)blockIdx.x * kStamps + (i)] = _t;                          \
         }                                                                                  \
     } while (0)
-#define DH_RSTAMP(A, i)                                                                    \
-    do {                                                                                   \
-        if ((A).stamps && threadIdx.x == 0)                                                \
-            (A).stamps[(size_t)blockIdx.x * kStamps + (i)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
 #else
 #define DH_STAMP(A, i) do {} while (0)
-#define DH_RSTAMP(A, i) do {} while (0)
 #endif
 
-__host__ __device__ constexpr int task_lds_doubles(int N, int tpt) {
-    // (T2,T3)[N] u[N] T4[N] | reduction [4][waves] | K, mkt, sse, bad [kTileMax] |
-    // call, perm, clamp list [kTileMax] ints + count (rounded to whole 16-B pairs)
-    return 4 * N + 4 * (tpt / 64) + 4 * kTileMax + ((3 * kTileMax + 4) / 2 + 1) / 2 * 2;
+__host__ __device__ inline int tabs_per_p(const PriceArgs& A) { return A.paired ? 1 : A.n_groups; }
+
+__device__ __forceinline__ double option_strike(const PriceArgs& A, int m, double S0) {
+    const double Kin = A.K[m];
+    return (A.strike_mode == DH_STRIKE_PCT_SPOT) ? Kin * S0 / 100.0 : Kin;
+}
+
+// ----------------------------------------------------------------------------------------------
+// table kernel
+// ----------------------------------------------------------------------------------------------
+// per-table constants broadcast through LDS (computed by the first wave of the table)
+constexpr int kTabC = 6 + 16;   // a, b, e^b, e^a, 2/(b-a), pi/(b-a) | CfConsts (16 doubles)
+static_assert(sizeof(dh::CfConsts) == 16 * sizeof(double), "CfConsts layout");
+
+#ifndef DH_TABLE_WAVES
+#define DH_TABLE_WAVES 1    // occupancy hint (min waves per SIMD) for the register allocator
+#endif
+#ifndef DH_OPTION_WAVES
+#define DH_OPTION_WAVES 1
+#endif
+
+template <int TPT>
+__global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(PriceArgs A) {
+    constexpr int kTabs = kBlock / TPT;
+    constexpr int kWaves = TPT / 64;
+    __shared__ double red[kTabs][4][kWaves];
+    __shared__ double shc[kTabs][kTabC];
+    const int slot = threadIdx.x / TPT;
+    const int t = threadIdx.x % TPT;
+    const int lane = threadIdx.x & 63;
+    const int wv = t >> 6;
+    const int N = A.N;
+    const int tpp = tabs_per_p(A);
+    const int64_t n_q = A.np * tpp;
+    const int64_t q = (int64_t)blockIdx.x * kTabs + __builtin_amdgcn_readfirstlane(slot);
+    const bool active = q < n_q;
+    const int64_t p = A.p0 + (active ? q / tpp : 0);
+    const int g = active ? (int)(q % tpp) : 0;
+    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
+    const double T = !active ? 1.0 : (A.paired ? A.T[p] : A.group_T[g]);
+
+    if (wv == 0) {   // truncation range and CF constants once per table
+        double a, b;
+        dh::trunc_unclamped(P, T, A.L, a, b);            // double_heston.py:100-132
+        const dh::CfConsts CC = dh::cf_consts(P, T);
+        if (lane == 0) {
+            double* c = shc[slot];
+            c[0] = a;
+            c[1] = b;
+            c[2] = exp(b);
+            c[3] = exp(a);
+            c[4] = 2.0 / (b - a);
+            c[5] = dh::kPi / (b - a);
+            const double* cc = (const double*)&CC;
+            for (int i = 0; i < 16; ++i) c[6 + i] = cc[i];
+        }
+    }
+    __syncthreads();
+    const double* c = shc[slot];
+    const double a = c[0], b = c[1], eb = c[2], ea = c[3], scale = c[4], piba = c[5];
+    dh::CfConsts CC;
+    {
+        double* cc = (double*)&CC;
+        for (int i = 0; i < 16; ++i) cc[i] = c[6 + i];
+    }
+    const double ba = b - a;
+    double* tw = A.table + (active ? q : 0) * (int64_t)N;
+    double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
+    if (active) {
+        for (int k = t; k < N; k += TPT) {
+            const double u = k * piba;                       // k pi / (b - a)
+            const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+            tw[k] = w;
+            if (k == 0) {
+                w0 = 0.5 * w;
+                continue;
+            }
+            double sb, cb;
+            dh::dsincos(u * ba, &sb, &cb);
+            const double T2 = w * P.S0 * dh::drcp(1.0 + u * u);
+            const double T4 = w * dh::drcp(u);
+            c0 += T2 * eb * (cb + u * sb);
+            c1 += T4 * sb;
+            c5 += T2 * ea;
+        }
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+        c0 += __shfl_xor(c0, off, 64);
+        c1 += __shfl_xor(c1, off, 64);
+        c5 += __shfl_xor(c5, off, 64);
+        w0 += __shfl_xor(w0, off, 64);
+    }
+    if (lane == 0) {
+        red[slot][0][wv] = c0;
+        red[slot][1][wv] = c1;
+        red[slot][2][wv] = c5;
+        red[slot][3][wv] = w0;
+    }
+    __syncthreads();
+    if (active && t == 0) {
+        double sm[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < 4; ++j)
+            for (int i = 0; i < kWaves; ++i) sm[j] += red[slot][j][i];
+        double* cs = A.consts + q * kConsts;
+        cs[0] = sm[0];
+        cs[1] = sm[1];
+        cs[2] = sm[2];
+        cs[3] = sm[3];
+        cs[4] = a;
+        cs[5] = b;
+        cs[6] = eb;
+        cs[7] = ea;
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// option kernel helpers
+// ----------------------------------------------------------------------------------------------
+struct Consts {
+    double c0, c1, c5, w0, a, b, eb, ea;
+};
+
+// sum' of one option from the table constants and its angle sums (k = 0 term:
+// chi_0 = e^d - e^c, psi_0 = d - c, double_heston.py:142-143,154-155).
+__device__ __forceinline__ double option_sum(const Consts& C, bool is_call, double S0, double K,
+                                             double xK, double exK, double s2, double s4) {
+    const double v0 = is_call ? (S0 * (C.eb - exK) - K * (C.b - xK))
+                              : (K * (xK - C.a) - S0 * (exK - C.ea));
+    const double cst = is_call ? (C.c0 - K * C.c1) : C.c5;
+    return cst + C.w0 * v0 - exK * s2 + K * s4;
+}
+
+// Angle sums of up to kR options on lanes k = k1, k1 + G, ...:
+//   s2_j = sum_k T2_k cos(k th_j) + T3_k sin(k th_j),  s4_j = sum_k T4_k sin(k th_j)
+// the angle u_k (xK_j - a) advances by the option's e^{i G th_j} rotation (cs, ss: staged once
+// per option), with an exact sincos re-anchor every kAnchor steps; one (T2, T3) ds_read_b128 and
+// one T4 read serve all kR options.
+__device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double (&dx)[kR],
+                                             const double (&cs)[kR], const double (&ss)[kR],
+                                             const double* tu, const double2* t23,
+                                             const double* t4, double (&s2)[kR],
+                                             double (&s4)[kR]) {
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+        s2[j] = 0.0;
+        s4[j] = 0.0;
+    }
+    if (k1 >= N) return;
+    double cx[kR], sx[kR];
+    const double u1 = tu[k1];
+#pragma unroll
+    for (int j = 0; j < kR; ++j) dh::dsincos(u1 * dx[j], &sx[j], &cx[j]);
+    int n = 0;
+    for (int k = k1; k < N; k += G, ++n) {
+        if (n == kAnchor) {
+            const double uk = tu[k];
+#pragma unroll
+            for (int j = 0; j < kR; ++j) dh::dsincos(uk * dx[j], &sx[j], &cx[j]);
+            n = 0;
+        }
+        const double2 a23 = t23[k];
+        const double a4 = t4[k];
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+            s2[j] = fma(a23.x, cx[j], s2[j]);
+            s2[j] = fma(a23.y, sx[j], s2[j]);
+            s4[j] = fma(a4, sx[j], s4[j]);
+            const double cn = cx[j] * cs[j] - sx[j] * ss[j];
+            sx[j] = sx[j] * cs[j] + cx[j] * ss[j];
+            cx[j] = cn;
+        }
+    }
+}
+
+// Per-term path for a clamp-widened option: own range [a, b], own u grid, CF per term (fast
+// exponent form) and the generic chi/psi (double_heston.py:141-158,160-192).  Lane share of
+// the sum' over k = k_first, k_first + k_step, ...
+__device__ __forceinline__ double clamped_term_sum(const Params& P, double T, double K, double xK,
+                                                   double a, double b, bool is_call, int k_first,
+                                                   int k_step, int N) {
+    const dh::CfConsts CC = dh::cf_consts(P, T);
+    const double ba = b - a;
+    const double scale = 2.0 / ba;
+    double acc = 0.0;
+    for (int k = k_first; k < N; k += k_step) {
+        const double u = k * dh::kPi / ba;
+        const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+        double chi, psi;
+        if (is_call) dh::cos_coeffs(k, xK, b, a, b, chi, psi);
+        else dh::cos_coeffs(k, a, xK, a, b, chi, psi);
+        const double V = is_call ? (P.S0 * chi - K * psi) : (K * psi - P.S0 * chi);
+        acc += (k == 0 ? 0.5 : 1.0) * w * V;
+    }
+    return acc;
 }
 
 __device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int col, double mk,
@@ -106,10 +305,10 @@ __device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int 
 }
 
 // Fixed-order loss partial of one task (wave 0 of the task).  Hand-off to the last task of param
-// set p without fences (MI355X_MICROARCH.md, "Valid forms", first table row): the storing lane
-// writes its partial with agent-scope (sc1, write-through) stores, drains them with
-// s_waitcnt vmcnt(0), then adds to p's counter; the lane whose add returns n_tiles - 1 reads every
-// partial of p with sc1 loads, sums them in tile order and resets the counter for the next launch.
+// set p without fences (MI355X_MICROARCH.md, "Valid forms", first table row): one lane writes
+// the partial with agent-scope (sc1, write-through) stores, drains them with s_waitcnt vmcnt(0),
+// then adds to p's counter; in the wave whose add returns n_tiles - 1 every lane reads partials
+// of p with sc1 loads, the wave sums them in a fixed order and resets the counter.
 __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t task, int nopt,
                                           int t, const double* lsse, const double* lbad) {
     double s = 0.0, f = 0.0;
@@ -131,7 +330,6 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     }
     old = __shfl(old, 0, 64);
     if (old != (unsigned)A.n_tiles - 1u) return;
-    // last arriver: the whole wave reads the partials of p (lane-strided, sc1), fixed order
     double acc = 0.0, bad = 0.0;
     for (int j = t; j < A.n_tiles; j += 64) {
         acc += __hip_atomic_load(&A.part_sse[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -148,9 +346,179 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     }
 }
 
+__host__ __device__ constexpr int option_lds_doubles(int N, int opt_cap) {
+    // (T2,T3)[N] T4[N] u[N] | K, mkt, sse, bad, xK, e^xK, cos/sin step [opt_cap] |
+    // call, perm, clamp [opt_cap] ints + clamp count, rounded to whole 16-byte pairs
+    return 4 * N + 8 * opt_cap + ((3 * opt_cap + 1 + 3) / 4) * 2;
+}
+
 // ----------------------------------------------------------------------------------------------
-// exact per-term path (validation mode): own truncation range, own u grid, CF per term, the
-// reference's operation order (double_heston.py:160-192).  Lane share of sum_k' Re(phi e^{-iua}) V_k.
+// option kernel
+// ----------------------------------------------------------------------------------------------
+template <int TPT>
+__global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(PriceArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int kTasks = kBlock / TPT;
+    const int slot = threadIdx.x / TPT;
+    const int t = threadIdx.x % TPT;
+    const int N = A.N;
+    const int64_t n_tasks = A.paired ? A.np : A.np * (int64_t)A.n_tiles;
+    // the task index is wave-uniform: make that visible so per-task values live in SGPRs
+    const int64_t task_l = (int64_t)blockIdx.x * kTasks + __builtin_amdgcn_readfirstlane(slot);
+    const bool active = task_l < n_tasks;
+    const int64_t p = A.p0 + (active ? (A.paired ? task_l : task_l / A.n_tiles) : 0);
+    const int tile = (active && !A.paired) ? (int)(task_l % A.n_tiles) : 0;
+    const int64_t task = A.paired ? p : p * A.n_tiles + tile;       // global task id
+    DH_STAMP(A, 0);
+
+    const int cap = A.opt_cap;
+    double* base = smem + (size_t)slot * option_lds_doubles(N, cap);
+    double2* t23 = (double2*)base;
+    double* t4 = base + 2 * N;
+    double* tu = base + 3 * N;
+    double* lK = base + 4 * N;
+    double* lmkt = lK + cap;
+    double* lsse = lmkt + cap;
+    double* lbad = lsse + cap;
+    double* lxK = lbad + cap;                          // log(K / S0)
+    double* lexK = lxK + cap;                          // e^{log(K / S0)}
+    double* lcs = lexK + cap;                          // cos / sin of the G-step rotation
+    double* lss = lcs + cap;
+    int* lcall = (int*)(lss + cap);
+    int* lperm = lcall + cap;
+    int* lclamp = lperm + cap;                         // [cap] clamped option indices
+    int* ncl = lclamp + cap;                           // [1] count
+
+    int opt0 = 0, nopt = 0, g = 0;
+    if (active) {
+        if (A.paired) {
+            opt0 = (int)p;
+            nopt = 1;
+        } else {
+            const int2 tl = A.tiles[tile];
+            opt0 = tl.x;
+            nopt = tl.y;
+            g = A.tile_group[tile];
+        }
+    }
+    // lanes: groups of kR options on G lanes each
+    const int R = min(kR, max(nopt, 1));
+    const int ngroups = (nopt + R - 1) / R;
+    int G = 1;
+    while (G * 2 <= TPT / max(ngroups, 1) && G < 64) G *= 2;
+    while (G > 1 && G / 2 >= N - 1) G /= 2;                 // no more lanes than terms k >= 1
+
+    const int64_t q = (p - A.p0) * tabs_per_p(A) + g;
+    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
+    Consts C{0.0, 0.0, 0.0, 0.0, 0.0, 1.0, 1.0, 1.0};
+    if (active) {
+        const double* cs = A.consts + q * kConsts;
+        C = Consts{cs[0], cs[1], cs[2], cs[3], cs[4], cs[5], cs[6], cs[7]};
+    }
+    const double ba = C.b - C.a;
+    if (t == 0) *ncl = 0;
+    // stage the (p, g) table, expanded to u, (T2, T3), T4 (same expressions as the table
+    // kernel's k-sums), and per-option data: log(K/S0), e^{xK}, the clamp test
+    // (double_heston.py:135-137) and the G-step rotation of each option
+    if (active) {
+        const double* tw = A.table + q * (int64_t)N;
+        const double piba = dh::kPi / ba;
+        for (int k = t; k < N; k += TPT) {
+            const double w = tw[k];
+            const double u = k * piba;
+            const double T2 = k == 0 ? 0.0 : w * P.S0 * dh::drcp(1.0 + u * u);
+            t23[k] = make_double2(T2, T2 * u);
+            t4[k] = k == 0 ? 0.0 : w * dh::drcp(u);
+            tu[k] = u;
+        }
+        const bool pct = A.strike_mode == DH_STRIKE_PCT_SPOT;
+        const double ustep = G * dh::kPi / ba;
+        for (int i = t; i < nopt; i += TPT) {
+            const double Kin = A.K[opt0 + i];
+            const double K = pct ? Kin * P.S0 / 100.0 : Kin;
+            const double xK = log(K / P.S0);                         // double_heston.py:162
+            lK[i] = K;
+            lmkt[i] = A.mkt ? A.mkt[opt0 + i] : 0.0;
+            lcall[i] = A.call[opt0 + i];
+            lperm[i] = A.perm[opt0 + i];
+            lxK[i] = xK;
+            lexK[i] = exp(xK);
+            const bool cl = xK - 0.1 < C.a || xK + 0.1 > C.b;
+            double ss, cs;
+            dh::dsincos(ustep * (cl ? 0.0 : xK - C.a), &ss, &cs);
+            lcs[i] = cs;
+            lss[i] = cl ? NAN : ss;                                  // NaN marks clamped
+        }
+    }
+    const double T = active ? A.T[opt0] : 1.0;
+    const double disc = exp(-P.r * T);
+    __syncthreads();
+    DH_STAMP(A, 1);
+
+    const int groups_per_pass = TPT / G;
+    for (int pass = 0; pass < ngroups; pass += groups_per_pass) {
+        const int gi = pass + t / G;
+        const int gl = t % G;
+        const bool gvalid = active && gi < ngroups;
+        double dx[kR], cs[kR], ss[kR];
+        bool use[kR];
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+            const int oi = gi * R + j;
+            const bool in = gvalid && j < R && oi < nopt;
+            const double sj = in ? lss[oi] : 0.0;
+            const bool clamped = in && isnan(sj);
+            if (clamped && gl == 0) lclamp[atomicAdd(ncl, 1)] = oi;   // priced below
+            use[j] = in && !clamped;
+            dx[j] = use[j] ? lxK[oi] - C.a : 0.0;
+            cs[j] = use[j] ? lcs[oi] : 1.0;
+            ss[j] = use[j] ? sj : 0.0;
+        }
+        double s2[kR], s4[kR];
+        angle_sums_r(1 + gl, G, N, dx, cs, ss, tu, t23, t4, s2, s4);
+        for (int off = 1; off < G; off <<= 1) {
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {
+                s2[j] += __shfl_xor(s2[j], off, 64);
+                s4[j] += __shfl_xor(s4[j], off, 64);
+            }
+        }
+        if (gl == 0) {
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {
+                if (!use[j]) continue;
+                const int oi = gi * R + j;
+                const double sum = option_sum(C, lcall[oi] != 0, P.S0, lK[oi], lxK[oi], lexK[oi],
+                                              s2[j], s4[j]);
+                record_price(A, p, lperm[oi], lmkt[oi], oi, disc * sum, lsse, lbad);
+            }
+        }
+    }
+    // clamp-widened options (double_heston.py:135-137): per-term path on each option's own
+    // range, one wave per option (no barrier inside: trip counts may differ between tasks)
+    __syncthreads();
+    const int n_cl = active ? *ncl : 0;
+    for (int c = t >> 6; c < n_cl; c += TPT / 64) {
+        const int oi = lclamp[c];
+        const double x = lxK[oi];
+        const double a = (x - 0.1 < C.a) ? x - 0.1 : C.a;      // Python min/max
+        const double b = (x + 0.1 > C.b) ? x + 0.1 : C.b;
+        double v = clamped_term_sum(P, T, lK[oi], x, a, b, lcall[oi] != 0, t & 63, 64, N);
+        for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+        if ((t & 63) == 0) record_price(A, p, lperm[oi], lmkt[oi], oi, disc * v, lsse, lbad);
+    }
+    DH_STAMP(A, 2);
+
+    // ---- loss: fixed-order per-task partial, last arriver finalises the param set ----
+    if (A.part_sse) {
+        __syncthreads();
+        if (active && t < 64) task_loss(A, p, task, nopt, t, lsse, lbad);
+    }
+    DH_STAMP(A, 3);
+}
+
+// ----------------------------------------------------------------------------------------------
+// validation path: reference operation order (double_heston.py:160-192), one wave per option
 // ----------------------------------------------------------------------------------------------
 __device__ __forceinline__ double exact_term_sum(const Params& P, double T, double K, double xK,
                                                  double a, double b, bool is_call, int k_first,
@@ -175,19 +543,14 @@ __device__ __forceinline__ double exact_term_sum(const Params& P, double T, doub
     return acc;
 }
 
-__device__ __forceinline__ double option_strike(const PriceArgs& A, int m, double S0) {
-    const double Kin = A.K[m];
-    return (A.strike_mode == DH_STRIKE_PCT_SPOT) ? Kin * S0 / 100.0 : Kin;
-}
-
-// Validation kernel: one wave per (param set, option); prices only (loss via loss_from_prices).
-__global__ __launch_bounds__(kBlock) void cos_exact_kernel(PriceArgs A, int M, double* prices) {
+__global__ __launch_bounds__(kBlock) void cos_exact_kernel(PriceArgs A, double* prices) {
     const int64_t item = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
+    const int M = A.M;
     const int64_t n_items = A.paired ? A.P : A.P * (int64_t)M;
     if (item >= n_items) return;                       // whole wave exits together
     const int64_t p = A.paired ? item : item / M;
-    const int m = A.paired ? (int)item : (int)(item % M);
+    const int m = A.paired ? (int)p : (int)(item % M);
     const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
     const double T = A.T[m];
     const double K = option_strike(A, m, P.S0);
@@ -202,20 +565,20 @@ __global__ __launch_bounds__(kBlock) void cos_exact_kernel(PriceArgs A, int M, d
     if (lane == 0) {
         const double price = exp(-P.r * T) * acc;
         if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
-        if (prices) prices[p * M + m] = price;
+        if (prices) prices[A.paired ? p : p * M + m] = price;
     }
 }
 
 // Loss sums from a [P][M] price buffer (validation mode): one wave per param set, fixed order.
 __global__ void loss_from_prices_kernel(const double* __restrict__ prices,
-                                        const double* __restrict__ mkt, int M, int S,
+                                        const double* __restrict__ mkt, int M, int64_t S,
                                         double* __restrict__ sse, int* __restrict__ n_bad) {
-    const int s = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+    const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (s >= S) return;
     double acc = 0.0, bad = 0.0;
     for (int m = lane; m < M; m += 64) {
-        const double pr = prices[(int64_t)s * M + m];
+        const double pr = prices[s * M + m];
         const double rel = (pr - mkt[m]) / mkt[m];
         acc += rel * rel;
         bad += (isnan(pr) || isinf(pr) || pr <= 0.0) ? 1.0 : 0.0;
@@ -231,312 +594,8 @@ __global__ void loss_from_prices_kernel(const double* __restrict__ prices,
 }
 
 // ----------------------------------------------------------------------------------------------
-// table build: COS table of (p, T, [a, b]) into LDS + the four k-sums, reduced in fixed order.
-// w_k = Re(phi(u_k) e^{-i u_k a}) 2/(b-a);  T2 = w S0/(1+u^2), T3 = T2 u, T4 = w/u   (k >= 1)
-// c0 = sum T2 e^b (cos(u(b-a)) + u sin(u(b-a)))   (call constant)
-// c1 = sum T4 sin(u(b-a))                          (call constant, times K)
-// c5 = sum T2 e^a                                  (put constant)
-// w0 = w_0 / 2                                     (k = 0 term weight)
-// Must be reached by every thread of the block (contains a barrier).
+// building blocks behind the reference's public methods
 // ----------------------------------------------------------------------------------------------
-struct Consts {
-    double c0, c1, c5, w0, eb, ea;
-};
-
-template <int TPT>
-__device__ __forceinline__ Consts build_table(const Params& P, double T, double a, double b,
-                                              bool work, int N, int t, double* tu, double2* t23,
-                                              double* t4, double* red) {
-    constexpr int kWaves = TPT / 64;
-    const int lane = threadIdx.x & 63;
-    const int wv = t >> 6;
-    const double ba = b - a;
-    const double scale = 2.0 / ba;
-    const double eb = exp(b), ea = exp(a);
-    const dh::CfConsts CC = dh::cf_consts(P, T);
-    double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
-    if (work) {
-        for (int k = t; k < N; k += TPT) {
-            const double u = k * dh::kPi / ba;
-            const double w = dh::cf_phase_re(CC, u, T, a) * scale;
-            if (k == 0) {
-                w0 = 0.5 * w;
-                continue;
-            }
-            double sb, cb;
-            dh::dsincos(u * ba, &sb, &cb);
-            const double i1 = 1.0 / (1.0 + u * u);
-            const double T2 = w * P.S0 * i1;
-            const double T4 = w * (1.0 / u);
-            tu[k] = u;
-            t23[k] = make_double2(T2, T2 * u);
-            t4[k] = T4;
-            c0 += T2 * eb * (cb + u * sb);
-            c1 += T4 * sb;
-            c5 += T2 * ea;
-        }
-    }
-    for (int off = 1; off < 64; off <<= 1) {
-        c0 += __shfl_xor(c0, off, 64);
-        c1 += __shfl_xor(c1, off, 64);
-        c5 += __shfl_xor(c5, off, 64);
-        w0 += __shfl_xor(w0, off, 64);
-    }
-    if (lane == 0) {
-        red[0 * kWaves + wv] = c0;
-        red[1 * kWaves + wv] = c1;
-        red[2 * kWaves + wv] = c5;
-        red[3 * kWaves + wv] = w0;
-    }
-    __syncthreads();
-    Consts C{0.0, 0.0, 0.0, 0.0, eb, ea};
-    for (int i = 0; i < kWaves; ++i) {
-        C.c0 += red[0 * kWaves + i];
-        C.c1 += red[1 * kWaves + i];
-        C.c5 += red[2 * kWaves + i];
-        C.w0 += red[3 * kWaves + i];
-    }
-    return C;
-}
-
-// sum' of one option from the table constants and its angle sums (k = 0 term:
-// chi_0 = e^d - e^c, psi_0 = d - c, double_heston.py:142-143,154-155).
-__device__ __forceinline__ double option_sum(const Consts& C, bool is_call, double S0, double K,
-                                             double xK, double exK, double a, double b,
-                                             double s2, double s4) {
-    const double v0 = is_call ? (S0 * (C.eb - exK) - K * (b - xK))
-                              : (K * (xK - a) - S0 * (exK - C.ea));
-    const double cst = is_call ? (C.c0 - K * C.c1) : C.c5;
-    return cst + C.w0 * v0 - exK * s2 + K * s4;
-}
-
-constexpr int kR = 4;   // options carried per lane in phase 2 (independent rotation chains)
-
-// Angle sums of up to kR options on lanes k = k1, k1 + G, ...:
-//   s2_j = sum_k T2_k cos(k th_j) + T3_k sin(k th_j),  s4_j = sum_k T4_k sin(k th_j)
-// the angle u_k (xK_j - a) advances by an e^{i G th_j} rotation, exact re-anchor every kAnchor
-// steps; one (T2, T3) ds_read_b128 + one T4 read serve all kR options.
-__device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double (&dx)[kR],
-                                             double ba, const double* tu, const double2* t23,
-                                             const double* t4, double (&s2)[kR],
-                                             double (&s4)[kR]) {
-#pragma unroll
-    for (int j = 0; j < kR; ++j) {
-        s2[j] = 0.0;
-        s4[j] = 0.0;
-    }
-    if (k1 >= N) return;
-    double cx[kR], sx[kR], cs[kR], ss[kR];
-    const double ustep = G * dh::kPi / ba;
-    const double u1 = tu[k1];
-#pragma unroll
-    for (int j = 0; j < kR; ++j) {
-        dh::dsincos(u1 * dx[j], &sx[j], &cx[j]);
-        dh::dsincos(ustep * dx[j], &ss[j], &cs[j]);
-    }
-    int n = 0;
-    for (int k = k1; k < N; k += G, ++n) {
-        if (n == kAnchor) {
-            const double uk = tu[k];
-#pragma unroll
-            for (int j = 0; j < kR; ++j) dh::dsincos(uk * dx[j], &sx[j], &cx[j]);
-            n = 0;
-        }
-        const double2 a23 = t23[k];
-        const double a4 = t4[k];
-#pragma unroll
-        for (int j = 0; j < kR; ++j) {
-            s2[j] = fma(a23.x, cx[j], s2[j]);
-            s2[j] = fma(a23.y, sx[j], s2[j]);
-            s4[j] = fma(a4, sx[j], s4[j]);
-            const double cn = cx[j] * cs[j] - sx[j] * ss[j];
-            sx[j] = sx[j] * cs[j] + cx[j] * ss[j];
-            cx[j] = cn;
-        }
-    }
-}
-
-#ifndef DH_MIN_WAVES
-#define DH_MIN_WAVES 1     // occupancy hint (waves per SIMD) for the register allocator
-#endif
-
-template <int TPT>
-__global__ __launch_bounds__(kBlock, DH_MIN_WAVES) void cos_price_kernel(PriceArgs A) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int kTasks = kBlock / TPT;
-    const int slot = threadIdx.x / TPT;
-    const int t = threadIdx.x % TPT;
-    const int N = A.N;
-    const int64_t n_tasks = A.paired ? A.P : A.P * (int64_t)A.n_tiles;
-    // the task index is wave-uniform: make that visible so params live in SGPRs
-    const int64_t task = (int64_t)blockIdx.x * kTasks + __builtin_amdgcn_readfirstlane(slot);
-    const bool active = task < n_tasks;
-    const int64_t p = active ? (A.paired ? task : task / A.n_tiles) : 0;
-    const int tile = active ? (A.paired ? 0 : (int)(task % A.n_tiles)) : 0;
-    DH_RSTAMP(A, 0);
-    DH_STAMP(A, 1);
-
-    // LDS per task: (T2,T3)[N] | u[N] | T4[N] | reduction | option data | loss | clamp list
-    double* base = smem + (size_t)slot * task_lds_doubles(N, TPT);
-    double2* t23 = (double2*)base;
-    double* tu = base + 2 * N;
-    double* t4 = base + 3 * N;
-    double* red = base + 4 * N;
-    double* lK = red + 4 * (TPT / 64);                 // [kTileMax] strikes
-    double* lmkt = lK + kTileMax;                      // [kTileMax] market prices
-    double* lsse = lmkt + kTileMax;                    // [kTileMax]
-    double* lbad = lsse + kTileMax;                    // [kTileMax]
-    int* lcall = (int*)(lbad + kTileMax);              // [kTileMax]
-    int* lperm = lcall + kTileMax;                     // [kTileMax]
-    int* lclamp = lperm + kTileMax;                    // [kTileMax] clamped option indices
-    int* ncl = lclamp + kTileMax;                      // [1]
-    int* nclmax = (int*)(smem + (size_t)kTasks * task_lds_doubles(N, TPT));   // [1] block max
-
-    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
-    int opt0 = 0, nopt = 0;
-    if (active) {
-        if (A.paired) {
-            opt0 = (int)p;
-            nopt = 1;
-        } else {
-            const int2 tl = A.tiles[tile];
-            opt0 = tl.x;
-            nopt = tl.y;
-        }
-    }
-    // prefetch this tile's option data (first chunk in registers across the truncation math)
-    const bool pf = active && t < nopt;
-    const double pK = pf ? A.K[opt0 + t] : 0.0;
-    const double pM = (pf && A.mkt) ? A.mkt[opt0 + t] : 0.0;
-    const int pC = pf ? A.call[opt0 + t] : 0;
-    const int pP = pf ? A.perm[opt0 + t] : 0;
-    if (t == 0) *ncl = 0;
-    if (threadIdx.x == 0) *nclmax = 0;
-    const double T = active ? A.T[opt0] : 1.0;
-    double a0, b0;
-    dh::trunc_unclamped(P, T, A.L, a0, b0);
-    const double ba0 = b0 - a0;
-    const double disc = exp(-P.r * T);
-    const bool pct = A.strike_mode == DH_STRIKE_PCT_SPOT;
-    if (pf) {
-        lK[t] = pct ? pK * P.S0 / 100.0 : pK;
-        lmkt[t] = pM;
-        lcall[t] = pC;
-        lperm[t] = pP;
-    }
-    for (int i = t + TPT; active && i < nopt; i += TPT) {
-        const double Kin = A.K[opt0 + i];
-        lK[i] = pct ? Kin * P.S0 / 100.0 : Kin;
-        lmkt[i] = A.mkt ? A.mkt[opt0 + i] : 0.0;
-        lcall[i] = A.call[opt0 + i];
-        lperm[i] = A.perm[opt0 + i];
-    }
-    DH_STAMP(A, 2);
-
-    // One table-build site for both passes (a second inlined copy of the CF costs ~80 VGPRs):
-    //   it = 0   table of (p, T) on the un-clamped range, then every option of the tile;
-    //   it >= 1  table rebuilt on the widened range of the (it-1)-th clamped option
-    //            (double_heston.py:135-137), then that option alone.
-    // The trip count is block-uniform (max over the block's tasks) because of the barriers.
-    int n_iter = 1;
-    for (int it = 0; it < n_iter; ++it) {
-        bool work = active;
-        int oi1 = 0;
-        double a = a0, b = b0, K1 = P.S0, xK1 = 0.0;
-        if (it > 0) {
-            work = active && it - 1 < *ncl;
-            oi1 = work ? lclamp[it - 1] : 0;
-            K1 = work ? lK[oi1] : P.S0;
-            xK1 = log(K1 / P.S0);
-            a = (xK1 - 0.1 < a0) ? xK1 - 0.1 : a0;          // Python min/max (:136-137)
-            b = (xK1 + 0.1 > b0) ? xK1 + 0.1 : b0;
-            __syncthreads();                                  // previous table readers are done
-        }
-        // table build (its barrier also publishes the prefetched option data on it = 0)
-        const Consts C = build_table<TPT>(P, T, a, b, work, N, t, tu, t23, t4, red);
-        if (it == 0) {
-            DH_STAMP(A, 3);
-            // ---- phase 2: option groups of kR options on G lanes each ----
-            const int R = min(kR, max(nopt, 1));
-            const int ngroups = (nopt + R - 1) / R;
-            int G = 1;
-            while (G * 2 <= TPT / max(ngroups, 1) && G < 64) G *= 2;
-            while (G > 1 && G / 2 >= N - 1) G /= 2;           // no more lanes than terms k >= 1
-            const int groups_per_pass = TPT / G;
-            for (int pass = 0; pass < ngroups; pass += groups_per_pass) {
-                const int gi = pass + t / G;
-                const int gl = t % G;
-                const bool gvalid = active && gi < ngroups;
-                double dx[kR], xK[kR];
-                bool use[kR];
-#pragma unroll
-                for (int j = 0; j < kR; ++j) {
-                    const int oi = gi * R + j;
-                    use[j] = gvalid && j < R && oi < nopt;
-                    const double K = use[j] ? lK[oi] : P.S0;
-                    xK[j] = log(K / P.S0);
-                    if (use[j] && (xK[j] - 0.1 < a0 || xK[j] + 0.1 > b0)) {   // widened range
-                        if (gl == 0) lclamp[atomicAdd(ncl, 1)] = oi;
-                        use[j] = false;
-                    }
-                    dx[j] = use[j] ? xK[j] - a0 : 0.0;
-                }
-                double s2[kR], s4[kR];
-                angle_sums_r(1 + gl, G, N, dx, ba0, tu, t23, t4, s2, s4);
-                for (int off = 1; off < G; off <<= 1) {
-#pragma unroll
-                    for (int j = 0; j < kR; ++j) {
-                        s2[j] += __shfl_xor(s2[j], off, 64);
-                        s4[j] += __shfl_xor(s4[j], off, 64);
-                    }
-                }
-                if (gl == 0) {
-#pragma unroll
-                    for (int j = 0; j < kR; ++j) {
-                        if (!use[j]) continue;
-                        const int oi = gi * R + j;
-                        const double sum = option_sum(C, lcall[oi] != 0, P.S0, lK[oi], xK[j],
-                                                      exp(xK[j]), a0, b0, s2[j], s4[j]);
-                        record_price(A, p, lperm[oi], lmkt[oi], oi, disc * sum, lsse, lbad);
-                    }
-                }
-            }
-            __syncthreads();
-            DH_STAMP(A, 4);
-            if (t == 0 && active) atomicMax(nclmax, *ncl);
-            __syncthreads();
-            n_iter = 1 + *nclmax;
-        } else {
-            double dx[kR] = {work ? xK1 - a : 0.0, 0.0, 0.0, 0.0};
-            double s2[kR], s4[kR];
-            if (work && t < 64) {
-                angle_sums_r(1 + t, 64, N, dx, b - a, tu, t23, t4, s2, s4);
-            } else {
-                s2[0] = 0.0;
-                s4[0] = 0.0;
-            }
-            for (int off = 1; off < 64; off <<= 1) {
-                s2[0] += __shfl_xor(s2[0], off, 64);
-                s4[0] += __shfl_xor(s4[0], off, 64);
-            }
-            if (work && t == 0) {
-                const double sum = option_sum(C, lcall[oi1] != 0, P.S0, K1, xK1, exp(xK1), a, b,
-                                              s2[0], s4[0]);
-                record_price(A, p, lperm[oi1], lmkt[oi1], oi1, disc * sum, lsse, lbad);
-            }
-        }
-    }
-
-    // ---- phase 3: fixed-order per-task loss partial, last arriver finalises the param set ----
-    DH_STAMP(A, 5);
-    if (A.part_sse) {
-        __syncthreads();
-        if (active && t < 64) task_loss(A, p, task, nopt, t, lsse, lbad);
-    }
-    DH_STAMP(A, 6);
-    DH_RSTAMP(A, 7);
-}
-
 __global__ void cf_kernel(const double* __restrict__ prm, const double* __restrict__ u, int n,
                           double tau, double* __restrict__ re, double* __restrict__ im) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -607,20 +666,24 @@ struct DevBuf {
     }
 };
 
-size_t lds_bytes(int N, int tpt) {
-    const int tasks = kBlock / tpt;
-    return ((size_t)tasks * task_lds_doubles(N, tpt) + 2) * sizeof(double);
-}
+int table_tpt(int N) { return N >= 256 ? 256 : (N >= 128 ? 128 : 64); }
 
-int pick_tpt(int N) { return N >= 256 ? 256 : (N >= 128 ? 128 : 64); }
+// option-kernel threads per task: enough lanes for ceil(nopt/kR) groups, LDS permitting
+int option_tpt(int max_nopt, int N, int cap) {
+    int tpt = max_nopt <= kR ? 64 : (max_nopt <= 4 * kR ? 128 : 256);
+    while (tpt < kBlock &&
+           (size_t)(kBlock / tpt) * option_lds_doubles(N, cap) * sizeof(double) > (size_t)kLdsMax)
+        tpt *= 2;
+    return tpt;
+}
 
 }  // namespace
 
 struct dh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, aux0, aux1, aux2,
-        aux3;
+    DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, aux0,
+        aux1, aux2, aux3;
     bool attr_set = false;
     int exact = 0;          // validation mode: every option through the per-term exact path
     int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
@@ -632,6 +695,8 @@ struct dh_surface {
     dh_ctx* ctx = nullptr;
     int M = 0;
     int n_tiles = 0;
+    int n_groups = 0;       // distinct maturities
+    int max_nopt = 0;       // largest tile
     int strike_mode = 0;
     bool has_mkt = false;
     double* K = nullptr;
@@ -640,6 +705,8 @@ struct dh_surface {
     int8_t* call = nullptr;
     int* perm = nullptr;
     int2* tiles = nullptr;
+    int* tile_group = nullptr;
+    double* group_T = nullptr;
 };
 
 namespace {
@@ -651,13 +718,12 @@ int set_device(dh_ctx* ctx) {
 
 int ensure_attrs(dh_ctx* ctx) {
     if (ctx->attr_set) return DH_OK;
-    const int lim = 160 * 1024;
-    HIP_TRY(hipFuncSetAttribute((const void*)cos_price_kernel<64>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lim));
-    HIP_TRY(hipFuncSetAttribute((const void*)cos_price_kernel<128>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lim));
-    HIP_TRY(hipFuncSetAttribute((const void*)cos_price_kernel<256>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+    HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<64>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<128>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<256>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     ctx->attr_set = true;
     return DH_OK;
 }
@@ -678,12 +744,11 @@ int launch_exact(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
     }
     const int64_t blocks = (n_items * 64 + kBlock - 1) / kBlock;
     if (blocks > 0x7fffffffLL) return fail(DH_E_ARG, "too many items for one launch");
-    hipLaunchKernelGGL(cos_exact_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, A, A.M,
-                       prices);
+    hipLaunchKernelGGL(cos_exact_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, A, prices);
     HIP_TRY(hipGetLastError());
     if (A.part_sse) {
-        const int S = (int)A.P;
-        hipLaunchKernelGGL(loss_from_prices_kernel, dim3((S * 64 + kBlock - 1) / kBlock),
+        const int64_t S = A.P;
+        hipLaunchKernelGGL(loss_from_prices_kernel, dim3((unsigned)((S * 64 + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, st, (const double*)prices, A.mkt, A.M, S, A.sse,
                            A.n_bad);
         HIP_TRY(hipGetLastError());
@@ -691,34 +756,56 @@ int launch_exact(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
     return DH_OK;
 }
 
-int launch_price(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
-    const int64_t n_tasks = A.paired ? A.P : A.P * (int64_t)A.n_tiles;
-    if (n_tasks == 0) return DH_OK;
-    if (A.exact) return launch_exact(ctx, A, st);
-    PriceArgs B = A;
-    if (ctx->stamps_on) {
-        const int tpb = kBlock / pick_tpt(A.N);
-        const int64_t nb = (n_tasks + tpb - 1) / tpb;
-        HIP_TRY(ctx->stamps.reserve((size_t)nb * kStamps * 8));
-        HIP_TRY(hipMemsetAsync(ctx->stamps.ptr, 0, (size_t)nb * kStamps * 8, st));
-        B.stamps = (unsigned long long*)ctx->stamps.ptr;
-        ctx->stamps_n = nb * kStamps;
-    }
+// Table kernel then option kernel per chunk of param sets; the chunk keeps the table workspace
+// within kTableBudget (L2/MALL-resident between the two launches).
+int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
+    const int64_t tasks_per_p = A0.paired ? 1 : A0.n_tiles;
+    if (A0.P * tasks_per_p == 0) return DH_OK;
+    if (A0.exact) return launch_exact(ctx, A0, st);
     int rc = ensure_attrs(ctx);
     if (rc) return rc;
-    const int tpt = pick_tpt(A.N);
-    const int tasks_per_block = kBlock / tpt;
-    const int64_t blocks = (n_tasks + tasks_per_block - 1) / tasks_per_block;
-    if (blocks > 0x7fffffffLL) return fail(DH_E_ARG, "too many tasks for one launch");
-    const size_t lds = lds_bytes(A.N, tpt);
-    if (lds > 160 * 1024) return fail(DH_E_ARG, "COS table does not fit in LDS");
-    dim3 grid((unsigned)blocks), block(kBlock);
-    switch (tpt) {
-        case 64: hipLaunchKernelGGL(cos_price_kernel<64>, grid, block, lds, st, B); break;
-        case 128: hipLaunchKernelGGL(cos_price_kernel<128>, grid, block, lds, st, B); break;
-        default: hipLaunchKernelGGL(cos_price_kernel<256>, grid, block, lds, st, B); break;
+    const int N = A0.N;
+    const int tpp = A0.paired ? 1 : A0.n_groups;
+    const size_t per_p = (size_t)tpp * ((size_t)N + kConsts) * sizeof(double);
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A0.P, kTableBudget / per_p));
+    HIP_TRY(ctx->table.reserve((size_t)chunk * tpp * N * sizeof(double)));
+    HIP_TRY(ctx->consts.reserve((size_t)chunk * tpp * kConsts * sizeof(double)));
+    const int t1 = table_tpt(N);
+    const int max_nopt = A0.paired ? 1 : A0.opt_cap;
+    const int t2 = option_tpt(max_nopt, N, A0.opt_cap);
+    const size_t lds2 = (size_t)(kBlock / t2) * option_lds_doubles(N, A0.opt_cap) * sizeof(double);
+    if (lds2 > (size_t)kLdsMax) return fail(DH_E_ARG, "COS table does not fit in LDS");
+    if (ctx->stamps_on) {
+        const int64_t nb = (chunk * tasks_per_p + kBlock / t2 - 1) / (kBlock / t2);
+        HIP_TRY(ctx->stamps.reserve((size_t)nb * kStamps * 8));
+        HIP_TRY(hipMemsetAsync(ctx->stamps.ptr, 0, (size_t)nb * kStamps * 8, st));
+        ctx->stamps_n = nb * kStamps;
     }
-    HIP_TRY(hipGetLastError());
+    for (int64_t p0 = 0; p0 < A0.P; p0 += chunk) {
+        PriceArgs A = A0;
+        A.p0 = p0;
+        A.np = std::min<int64_t>(chunk, A0.P - p0);
+        A.table = (double*)ctx->table.ptr;
+        A.consts = (double*)ctx->consts.ptr;
+        A.stamps = ctx->stamps_on ? (unsigned long long*)ctx->stamps.ptr : nullptr;
+        const int64_t n_q = A.np * tpp;
+        const int64_t b1 = (n_q + kBlock / t1 - 1) / (kBlock / t1);
+        const int64_t n_t = A.np * tasks_per_p;
+        const int64_t b2 = (n_t + kBlock / t2 - 1) / (kBlock / t2);
+        if (b1 > 0x7fffffffLL || b2 > 0x7fffffffLL) return fail(DH_E_ARG, "launch too large");
+        switch (t1) {
+            case 64: hipLaunchKernelGGL(cos_table_kernel<64>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
+            case 128: hipLaunchKernelGGL(cos_table_kernel<128>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
+            default: hipLaunchKernelGGL(cos_table_kernel<256>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
+        }
+        HIP_TRY(hipGetLastError());
+        switch (t2) {
+            case 64: hipLaunchKernelGGL(cos_option_kernel<64>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;
+            case 128: hipLaunchKernelGGL(cos_option_kernel<128>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;
+            default: hipLaunchKernelGGL(cos_option_kernel<256>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;
+        }
+        HIP_TRY(hipGetLastError());
+    }
     return DH_OK;
 }
 
@@ -773,7 +860,8 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->params, &ctx->out, &ctx->sse, &ctx->bad, &ctx->part_sse,
-                      &ctx->part_bad, &ctx->counter, &ctx->exact_prices, &ctx->stamps, &ctx->aux0,
+                      &ctx->part_bad, &ctx->counter, &ctx->exact_prices, &ctx->stamps, &ctx->table,
+                      &ctx->consts, &ctx->aux0,
                       &ctx->aux1, &ctx->aux2, &ctx->aux3})
         b->release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -842,10 +930,18 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
         if (mkt) sm[i] = mkt[perm[i]];
     }
     std::vector<int2> tiles;
+    std::vector<int> tile_group;
+    std::vector<double> group_T;
+    int max_nopt = 0;
     for (int i = 0; i < M;) {
         int j = i;
         while (j < M && sT[j] == sT[i]) ++j;
-        for (int s = i; s < j; s += kTileMax) tiles.push_back(make_int2(s, std::min(kTileMax, j - s)));
+        for (int s = i; s < j; s += kTileMax) {
+            tiles.push_back(make_int2(s, std::min(kTileMax, j - s)));
+            tile_group.push_back((int)group_T.size());
+            max_nopt = std::max(max_nopt, std::min(kTileMax, j - s));
+        }
+        group_T.push_back(sT[i]);
         i = j;
     }
     dh_surface* s = new (std::nothrow) dh_surface();
@@ -853,6 +949,8 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
     s->ctx = ctx;
     s->M = M;
     s->n_tiles = (int)tiles.size();
+    s->n_groups = (int)group_T.size();
+    s->max_nopt = max_nopt;
     s->strike_mode = strike_mode;
     s->has_mkt = mkt != nullptr;
     const size_t m8 = std::max<size_t>(1, (size_t)M) * 8;
@@ -866,6 +964,8 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
     alloc((void**)&s->call, std::max(1, M));
     alloc((void**)&s->perm, std::max<size_t>(1, (size_t)M) * 4);
     alloc((void**)&s->tiles, std::max<size_t>(1, tiles.size()) * sizeof(int2));
+    alloc((void**)&s->tile_group, std::max<size_t>(1, tile_group.size()) * sizeof(int));
+    alloc((void**)&s->group_T, std::max<size_t>(1, group_T.size()) * sizeof(double));
     if (e == hipSuccess && M > 0) {
         e = hipMemcpy(s->K, sK.data(), (size_t)M * 8, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(s->T, sT.data(), (size_t)M * 8, hipMemcpyHostToDevice);
@@ -875,6 +975,12 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
             e = hipMemcpy(s->perm, perm.data(), (size_t)M * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess)
             e = hipMemcpy(s->tiles, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(s->tile_group, tile_group.data(), tile_group.size() * sizeof(int),
+                          hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(s->group_T, group_T.data(), group_T.size() * sizeof(double),
+                          hipMemcpyHostToDevice);
     }
     if (e != hipSuccess) {
         dh_surface_destroy(s);
@@ -888,7 +994,7 @@ int dh_surface_destroy(dh_surface* s) {
     if (!s) return DH_OK;
     if (s->ctx) (void)hipSetDevice(s->ctx->device);
     for (void* p : {(void*)s->K, (void*)s->T, (void*)s->mkt, (void*)s->call, (void*)s->perm,
-                    (void*)s->tiles})
+                    (void*)s->tiles, (void*)s->tile_group, (void*)s->group_T})
         if (p) (void)hipFree(p);
     delete s;
     return DH_OK;
@@ -912,7 +1018,11 @@ static PriceArgs surface_args(const dh_surface* s, const double* d_params, int64
     A.mkt = s->mkt;
     A.perm = s->perm;
     A.tiles = s->tiles;
+    A.tile_group = s->tile_group;
+    A.group_T = s->group_T;
     A.n_tiles = s->n_tiles;
+    A.n_groups = s->n_groups;
+    A.opt_cap = ((s->max_nopt + 1) / 2) * 2;
     A.M = s->M;
     A.paired = 0;
     A.strike_mode = s->strike_mode;
@@ -1059,6 +1169,7 @@ int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const dou
     A.call = (const int8_t*)ctx->aux2.ptr;
     A.perm = (const int*)ctx->aux3.ptr;
     A.paired = 1;
+    A.opt_cap = 2;
     A.M = (int)P;
     A.exact = ctx->exact;
     A.strike_mode = DH_STRIKE_ABSOLUTE;
