@@ -137,6 +137,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
     const int g = active ? (int)(q % tpp) : 0;
     const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
     const double T = !active ? 1.0 : (A.paired ? A.T[p] : A.group_T[g]);
+    DH_STAMP(A, 4);
 
     if (wv == 0) {   // truncation range and CF constants once per table
         double a, b;
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
         }
     }
     __syncthreads();
+    DH_STAMP(A, 5);
     const double* c = shc[slot];
     const double a = c[0], b = c[1], eb = c[2], ea = c[3], scale = c[4], piba = c[5];
     dh::CfConsts CC;
@@ -183,6 +185,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             c5 += T2 * ea;
         }
     }
+    DH_STAMP(A, 6);
     for (int off = 1; off < 64; off <<= 1) {
         c0 += __shfl_xor(c0, off, 64);
         c1 += __shfl_xor(c1, off, 64);
@@ -210,6 +213,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
         cs[6] = eb;
         cs[7] = ea;
     }
+    DH_STAMP(A, 7);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -436,13 +440,14 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
         for (int i = t; i < nopt; i += TPT) {
             const double Kin = A.K[opt0 + i];
             const double K = pct ? Kin * P.S0 / 100.0 : Kin;
-            const double xK = log(K / P.S0);                         // double_heston.py:162
+            const double ratio = K / P.S0;
+            const double xK = dh::dlog(ratio);                       // double_heston.py:162
             lK[i] = K;
             lmkt[i] = A.mkt ? A.mkt[opt0 + i] : 0.0;
             lcall[i] = A.call[opt0 + i];
             lperm[i] = A.perm[opt0 + i];
             lxK[i] = xK;
-            lexK[i] = exp(xK);
+            lexK[i] = ratio;                                         // e^{xK} to an ulp
             const bool cl = xK - 0.1 < C.a || xK + 0.1 > C.b;
             double ss, cs;
             dh::dsincos(ustep * (cl ? 0.0 : xK - C.a), &ss, &cs);
@@ -483,7 +488,23 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
                 s4[j] += __shfl_xor(s4[j], off, 64);
             }
         }
-        if (gl == 0) {
+        // every lane of the group holds the (bitwise identical) sums: lane j finalises option j
+        if (G >= R) {
+            double m2 = s2[0], m4 = s4[0];
+            bool mu = use[0];
+#pragma unroll
+            for (int j = 1; j < kR; ++j) {
+                m2 = gl == j ? s2[j] : m2;
+                m4 = gl == j ? s4[j] : m4;
+                mu = gl == j ? use[j] : mu;
+            }
+            if (gl < R && mu) {
+                const int oi = gi * R + gl;
+                const double sum = option_sum(C, lcall[oi] != 0, P.S0, lK[oi], lxK[oi], lexK[oi],
+                                              m2, m4);
+                record_price(A, p, lperm[oi], lmkt[oi], oi, disc * sum, lsse, lbad);
+            }
+        } else if (gl == 0) {
 #pragma unroll
             for (int j = 0; j < kR; ++j) {
                 if (!use[j]) continue;
@@ -776,7 +797,8 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     const size_t lds2 = (size_t)(kBlock / t2) * option_lds_doubles(N, A0.opt_cap) * sizeof(double);
     if (lds2 > (size_t)kLdsMax) return fail(DH_E_ARG, "COS table does not fit in LDS");
     if (ctx->stamps_on) {
-        const int64_t nb = (chunk * tasks_per_p + kBlock / t2 - 1) / (kBlock / t2);
+        const int64_t nb = std::max((chunk * tasks_per_p + kBlock / t2 - 1) / (kBlock / t2),
+                                    (chunk * tpp + kBlock / t1 - 1) / (kBlock / t1));
         HIP_TRY(ctx->stamps.reserve((size_t)nb * kStamps * 8));
         HIP_TRY(hipMemsetAsync(ctx->stamps.ptr, 0, (size_t)nb * kStamps * 8, st));
         ctx->stamps_n = nb * kStamps;

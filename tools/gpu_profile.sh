@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round profile set, run ON THE GPU BOX (gpurun):  TAG=r01 tools/gpu_profile.sh
+#   1) rocprofv3 --kernel-trace --stats of the bench (per config, calibration leg off so every
+#      COS launch has the bench's request shape);
+#   2) PMC passes, one counter group per run, kernel-trace only (never with sys/runtime trace):
+#      FETCH_SIZE / WRITE_SIZE (separate passes, MI355X_MICROARCH.md) and the fp64 instruction mix.
+# Outputs under gpurun_out/prof/; tools/summarize_profiles.py turns them into profiles/<TAG>_*.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+TAG=${TAG:-r01}
+CONFIGS=${CONFIGS:-"c2 c3"}
+OUT=gpurun_out/prof
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null || exit 1
+for c in $CONFIGS; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o ${TAG}_${c}_stats --output-format csv \
+      -- python bench.py --config $c --steps 100 --warmup 10 --no-cpu --no-calib \
+      > $OUT/${TAG}_${c}_stats.log 2>&1 || { echo "stats $c failed rc=$?"; exit 1; }
+  echo "stats $c ok"
+  i=0
+  while IFS= read -r grp; do
+    [ -z "$grp" ] && continue
+    i=$((i+1))
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $OUT -o ${TAG}_${c}_pmc$i --output-format csv \
+        -- python bench.py --config $c --steps 20 --warmup 3 --no-cpu --no-calib \
+        > $OUT/${TAG}_${c}_pmc$i.log 2>&1 || { echo "pmc $c pass $i failed rc=$?"; exit 1; }
+    echo "pmc $c pass $i ($grp) ok"
+  done <<EOG
+FETCH_SIZE
+WRITE_SIZE
+SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU GRBM_GUI_ACTIVE
+SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU
+EOG
+done
+echo done

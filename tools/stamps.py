@@ -3,7 +3,9 @@
 Usage:  make -C option-pricing-ffn-lbfgs_amd/csrc stamps
         python tools/stamps.py [--config c2] [--mode loss|price]
 Stamps per block of cos_option_kernel: [0] start, [1] table + option data staged,
-[2] options priced (incl. clamp path), [3] loss hand-off done.  s_memtime is per XCD, so only
+[2] options priced (incl. clamp path), [3] loss hand-off done; of the cos_table_kernel block with
+the same index: [4] start, [5] truncation range + CF constants ready, [6] CF loop done, [7] end.
+s_memtime is per XCD, so only
 differences inside one block are meaningful; read shares, not absolute lengths.
 """
 import argparse
@@ -40,6 +42,12 @@ def main():
         surf.price(host[1], cfg["N"])
     st = surf.ctx.read_stamps().astype(np.int64)
     surf.ctx.debug_stamps(False)
+    tb = st[st[:, 4] > 0]
+    print(f"{args.config} {args.mode}: table-kernel blocks {len(tb)}")
+    for nm, c in zip(["consts", "cf loop", "reduce"], [tb[:, 5] - tb[:, 4], tb[:, 6] - tb[:, 5],
+                                                      tb[:, 7] - tb[:, 6]]):
+        print(f"  {nm:8s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}  "
+              f"max {c.max():8.0f} cycles")
     st = st[st[:, 0] > 0]
     print(f"{args.config} {args.mode}: option-kernel blocks {len(st)}")
     for nm, c in zip(["stage", "options", "loss"], [st[:, 1] - st[:, 0], st[:, 2] - st[:, 1],

@@ -1,0 +1,121 @@
+"""Turn a round's rocprofv3 outputs (tools/gpu_profile.sh, merged into gpurun_out/prof/) into the
+committed evidence under profiles/:
+
+  profiles/<tag>_<config>_kernel_stats.csv   rocprofv3 --stats summary, verbatim
+  profiles/<tag>_<config>_pmc.csv            per-kernel medians of every PMC counter collected
+  profiles/pmc_traffic.json                  per config: HBM bytes per request (read by bench.py)
+  profiles/<tag>_summary.md                  the same numbers as a table
+
+HBM bytes follow MI355X_MICROARCH.md's rocprofv3 section: FETCH_SIZE and WRITE_SIZE come from
+separate passes and are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide coalesced
+read, so it is doubled.  A request is one cos_table_kernel + one cos_option_kernel launch.
+
+usage: python tools/summarize_profiles.py --tag r01 [--src gpurun_out/prof]
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = ("cos_table_kernel", "cos_option_kernel")
+
+
+def short(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return None
+
+
+def median(v):
+    v = sorted(v)
+    n = len(v)
+    return v[n // 2] if n % 2 else 0.5 * (v[n // 2 - 1] + v[n // 2])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default="r01")
+    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out", "prof"))
+    ap.add_argument("--configs", default="c2,c3")
+    args = ap.parse_args()
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    tpath = os.path.join(prof, "pmc_traffic.json")
+    traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
+    md = [f"# Profile summary {args.tag}", "",
+          "One request = cos_table_kernel + cos_option_kernel. Durations: rocprofv3 --kernel-trace "
+          "--stats average; counters: per-launch medians of separate --pmc passes.", ""]
+    for c in args.configs.split(","):
+        stats = os.path.join(args.src, f"{args.tag}_{c}_stats_kernel_stats.csv")
+        if not os.path.exists(stats):
+            print("missing", stats)
+            continue
+        shutil.copy(stats, os.path.join(prof, f"{args.tag}_{c}_kernel_stats.csv"))
+        avg = {}
+        for r in csv.DictReader(open(stats)):
+            k = short(r["Name"])
+            if k:
+                avg[k] = float(r["AverageNs"])
+        vals = collections.defaultdict(list)
+        for f in glob.glob(os.path.join(args.src, f"{args.tag}_{c}_pmc*_counter_collection.csv")):
+            for r in csv.DictReader(open(f)):
+                k = short(r["Kernel_Name"])
+                if k:
+                    vals[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+        med = {key: median(v) for key, v in vals.items()}
+        with open(os.path.join(prof, f"{args.tag}_{c}_pmc.csv"), "w", newline="") as fh:
+            w = csv.writer(fh)
+            w.writerow(["kernel", "counter", "median_per_launch", "launches"])
+            for (k, ctr), v in sorted(med.items()):
+                w.writerow([k, ctr, v, len(vals[(k, ctr)])])
+        per_kernel = {}
+        for k in KERNELS:
+            fetch = med.get((k, "FETCH_SIZE"))
+            write = med.get((k, "WRITE_SIZE"))
+            e = {"avg_ns": avg.get(k)}
+            if fetch is not None and write is not None:
+                e["fetch_bytes"] = 2.0 * fetch * 1024.0
+                e["write_bytes"] = write * 1024.0
+            f64 = [med.get((k, n)) for n in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
+                                             "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")]
+            if all(x is not None for x in f64):
+                # executed fp64 flops: 64 lanes per wave instruction, fma = 2
+                e["exec_fp64_flop"] = 64.0 * (2 * f64[0] + f64[1] + f64[2] + f64[3])
+                e["valu_insts"] = med.get((k, "SQ_INSTS_VALU"))
+            for n in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                      "SQ_BUSY_CYCLES", "SQ_WAVES"):
+                if (k, n) in med:
+                    e[n] = med[(k, n)]
+            per_kernel[k] = e
+        hbm = None
+        if all("fetch_bytes" in per_kernel[k] for k in KERNELS):
+            hbm = sum(per_kernel[k]["fetch_bytes"] + per_kernel[k]["write_bytes"] for k in KERNELS)
+        req_ns = sum(per_kernel[k]["avg_ns"] or 0.0 for k in KERNELS)
+        traffic[c] = {"round": args.tag, "hbm_bytes_per_launch": hbm, "request_avg_ns": req_ns,
+                      "kernels": per_kernel,
+                      "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->bytes, both kernels"}
+        md += [f"## {c}", "", "| kernel | avg us | fetch MB | write MB | exec fp64 GFLOP | "
+               "exec fp64 TFLOP/s | wait_any/wave_cycles |", "|---|---|---|---|---|---|---|"]
+        for k in KERNELS:
+            e = per_kernel[k]
+            t = (e["avg_ns"] or 0) * 1e-9
+            ef = e.get("exec_fp64_flop")
+            wa = (e["SQ_WAIT_ANY"] / e["SQ_WAVE_CYCLES"]) if e.get("SQ_WAVE_CYCLES") else None
+            md.append(f"| {k} | {t * 1e6:.2f} | {e.get('fetch_bytes', 0) / 1e6:.3f} | "
+                      f"{e.get('write_bytes', 0) / 1e6:.3f} | "
+                      f"{(ef or 0) / 1e9:.3f} | {(ef or 0) / t / 1e12 if t else 0:.2f} | "
+                      f"{'%.3f' % wa if wa is not None else '-'} |")
+        md += ["", f"request: {req_ns / 1e3:.2f} us, HBM/fabric bytes {hbm / 1e6 if hbm else 0:.3f} MB",
+               ""]
+    json.dump(traffic, open(tpath, "w"), indent=1)
+    open(os.path.join(prof, f"{args.tag}_summary.md"), "w").write("\n".join(md) + "\n")
+    print("\n".join(md))
+
+
+if __name__ == "__main__":
+    main()
