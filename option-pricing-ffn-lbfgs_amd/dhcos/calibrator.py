@@ -65,6 +65,9 @@ class CalibrationResult:
     message: str = ""
 
 
+# pickles name the reference's module (lbfgs_calibrator.py), see ../lbfgs_calibrator.py
+CalibrationResult.__module__ = "lbfgs_calibrator"
+
 def x_to_model(X: np.ndarray) -> np.ndarray:
     """Unconstrained x [..., 13] -> model params [..., 13] (exp / tanh / identity)."""
     X = np.asarray(X, dtype=np.float64)

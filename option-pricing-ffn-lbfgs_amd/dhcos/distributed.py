@@ -1,0 +1,204 @@
+"""Multi-GPU sharding of the hot path: one process per GPU, ``torch.distributed``
+(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for the CPU tests).  Nothing on the data path
+is exchanged: the shards are independent and each rank drives its own GPU.
+
+  * ``calibrate_sharded``: the starts of ``calibrate(maxiter, multi_start)`` are dealt
+    round-robin over the ranks (start s on rank s % world); each rank runs its starts in lockstep
+    on its own GPU, then ONE all-gather of a fixed-size record per start (status, fun, success,
+    nit, nfev, time, x[13], message bytes) gives every rank the whole table, and the best start is
+    chosen exactly as the reference does -- strict ``<`` over starts in start order
+    (lbfgs_calibrator.py:271-299).  Start x0s are drawn on rank 0 in start order from the global
+    ``np.random`` stream (the reference's only RNG consumer, :256) and broadcast, so the result
+    equals the single-process ``calibrate`` with the same RNG state.
+  * ``generate_sharded``: rank 0 draws every sample's random numbers in reference order
+    (synthetic_generator.py:98-141) and broadcasts them; rank r prices a contiguous block of
+    samples; one all-gather assembles the prices on every rank; rank 0 builds and saves the
+    reference output.
+
+Only collectives on small host-side records and (generator) the price block are used; the COS
+kernels never wait on another rank.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native
+from .calibrator import (CalibrationResult, DoubleHestonJumpCalibrator, N_PARAMS, run_starts)
+
+_MSG_BYTES = 64                        # SciPy messages are <= 52 characters
+_REC = 7 + N_PARAMS                    # status, start, fun, success, nit, nfev, t_rel, x[13]
+_REC_I64 = _REC + _MSG_BYTES // 8
+
+
+def _comm_device(group=None):
+    """Device on which collectives of this group take tensors (RCCL: the rank's GPU)."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _world(group=None):
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def _broadcast_f64(arr, shape, group=None):
+    """Broadcast a float64 array from rank 0 (bit-exact)."""
+    dev = _comm_device(group)
+    t = torch.empty(shape, dtype=torch.float64, device=dev)
+    if dist.get_rank(group) == 0:
+        t.copy_(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64).reshape(shape)))
+    dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    return t.cpu().numpy()
+
+
+def start_shard(n_starts: int, rank: int, world: int):
+    """Start indices owned by ``rank`` (round-robin keeps the guess types mixed per rank)."""
+    return list(range(rank, n_starts, world))
+
+
+def _encode(s, out, t0):
+    """Fixed-size int64 record of one start's outcome (doubles bit-cast, message as bytes)."""
+    rec = np.zeros(_REC_I64, dtype=np.int64)
+    d = np.zeros(_REC, dtype=np.float64)
+    d[1] = s
+    if out is not None:
+        res, t_done = out
+        d[0] = 1.0
+        d[2] = res.fun
+        d[3] = 1.0 if res.success else 0.0
+        d[4] = res.nit
+        d[5] = res.nfev
+        d[6] = t_done - t0
+        d[7:] = res.x
+        msg = str(res.message).encode("utf-8")[:_MSG_BYTES]
+        rec[_REC:] = np.frombuffer(msg.ljust(_MSG_BYTES, b"\0"), dtype=np.int64)
+    rec[:_REC] = d.view(np.int64)
+    return rec
+
+
+def _decode(rec):
+    d = rec[:_REC].view(np.float64)
+    if d[0] != 1.0:
+        return int(d[1]), None
+    msg = rec[_REC:].tobytes().rstrip(b"\0").decode("utf-8", "replace")
+    return int(d[1]), dict(fun=float(d[2]), success=bool(d[3]), nit=int(d[4]), nfev=int(d[5]),
+                           t_rel=float(d[6]), x=d[7:].copy(), message=msg)
+
+
+def gather_start_records(local, n_starts, group=None):
+    """All-gather the per-start records of every rank; returns [n_starts] decoded outcomes."""
+    rank, world = _world(group)
+    n_max = (n_starts + world - 1) // world
+    buf = np.zeros((n_max, _REC_I64), dtype=np.int64)
+    buf[:, :_REC] = np.full(_REC, -1.0).view(np.int64)      # padding rows: start index -1
+    for i, rec in enumerate(local):
+        buf[i] = rec
+    dev = _comm_device(group)
+    mine = torch.from_numpy(buf).to(dev)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    table = [None] * n_starts
+    for p in parts:
+        for row in p.cpu().numpy():
+            s, out = _decode(row)
+            if 0 <= s < n_starts:
+                table[s] = out
+    return table
+
+
+def calibrate_sharded(cal: DoubleHestonJumpCalibrator, maxiter: int = 300, multi_start: int = 3,
+                      *, group=None, x0s=None) -> CalibrationResult:
+    """``cal.calibrate(maxiter, multi_start)`` with the starts sharded over the process group.
+    Every rank returns the same ``CalibrationResult``."""
+    rank, world = _world(group)
+    if world == 1:
+        return cal.calibrate(maxiter=maxiter, multi_start=multi_start, x0s=x0s)
+    t0 = time.time()
+    if x0s is None and rank == 0:
+        x0s = [cal.get_initial_guess(guess_type=s % 3) for s in range(multi_start)]
+    x0s = _broadcast_f64(None if x0s is None else np.asarray(x0s), (multi_start, N_PARAMS),
+                         group)
+    mine = start_shard(multi_start, rank, world)
+    outcomes = run_starts(cal, [x0s[s] for s in mine], maxiter) if mine else []
+    local = [_encode(s, o, t0) for s, o in zip(mine, outcomes)]
+    table = gather_start_records(local, multi_start, group)
+
+    best, best_loss = None, np.inf
+    for s, out in enumerate(table):          # strict < in start order (:271)
+        if out is None:
+            continue
+        if out["fun"] < best_loss:
+            best_loss = out["fun"]
+            params = cal.transform_params(out["x"])
+            try:
+                model = cal._model_prices(params)
+            except _native.NativeError:
+                raise
+            except Exception:
+                continue
+            best = CalibrationResult(
+                date="", spot=cal.spot, risk_free=cal.risk_free_rate, parameters=params,
+                market_prices=cal.market_prices, model_prices=model,
+                market_options=cal.market_options, final_loss=out["fun"],
+                calibration_time=out["t_rel"], success=out["success"], iterations=out["nit"],
+                message=out["message"])
+    if best is None:
+        best = CalibrationResult(
+            date="", spot=cal.spot, risk_free=cal.risk_free_rate,
+            parameters={name: 0.0 for name in cal.param_names},
+            market_prices=cal.market_prices, model_prices=np.zeros_like(cal.market_prices),
+            market_options=cal.market_options, final_loss=np.inf,
+            calibration_time=time.time() - t0, success=False, iterations=0,
+            message="All optimization starts failed")
+    return best
+
+
+def sample_block(n: int, rank: int, world: int):
+    """Contiguous [lo, hi) block of samples owned by ``rank``."""
+    per = (n + world - 1) // world
+    lo = min(n, rank * per)
+    return lo, min(n, lo + per)
+
+
+def generate_sharded(n_samples: int = 500,
+                     save_path: str = "lbfgs_calibrations_synthetic.pkl", *, N: int = 128,
+                     as_arrays: bool = False, verbose: bool = True, group=None, price_fn=None,
+                     device=None):
+    """``generate_synthetic_calibrations`` with the pricing sharded over the process group.
+    Rank 0 returns (and saves) the reference output; other ranks return None."""
+    from . import generator as G
+
+    rank, world = _world(group)
+    price_fn = price_fn or (lambda p, s: G.price_grid(p, s, N=N, device=device))
+    n_opt = len(G.STRIKES_PCT) * len(G.MATURITIES)
+    width = 13 + 1 + n_opt
+    draws = None
+    if rank == 0:
+        params, spots, noise = G.draw_paths(n_samples)
+        draws = np.concatenate([params, spots[:, None], noise], axis=1)
+    if world > 1:
+        draws = _broadcast_f64(draws, (n_samples, width), group)
+    params, spots, noise = draws[:, :13], draws[:, 13], draws[:, 14:]
+    lo, hi = sample_block(n_samples, rank, world)
+    block = price_fn(params[lo:hi], spots[lo:hi]) if hi > lo else np.empty((0, n_opt))
+    if world > 1:
+        per = (n_samples + world - 1) // world
+        buf = np.zeros((per, n_opt))
+        buf[:hi - lo] = block
+        dev = _comm_device(group)
+        mine = torch.from_numpy(buf).to(dev)
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine, group=group)
+        model = np.concatenate([p.cpu().numpy() for p in parts])[:n_samples]
+    else:
+        model = block
+    if rank != 0:
+        return None
+    return G.assemble(params, spots, noise, model, save_path, as_arrays=as_arrays,
+                      verbose=verbose, N=N)

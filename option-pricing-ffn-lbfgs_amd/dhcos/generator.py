@@ -102,14 +102,21 @@ def generate_synthetic_calibrations(n_samples: int = 500,
                                     N: int = 128, device=None, as_arrays: bool = False,
                                     verbose: bool = True):
     """Generate ``n_samples`` synthetic calibrations (synthetic_generator.py:25-234)."""
+    params, spots, noise = draw_paths(n_samples)
+    model = price_grid(params, spots, N=N, device=device)
+    return assemble(params, spots, noise, model, save_path, as_arrays=as_arrays,
+                    verbose=verbose, N=N)
+
+
+def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose=True, N=128):
+    """Host part after pricing: noise, per-sample loss, output records (:141-183)."""
     say = print if verbose else (lambda *a, **k: None)
+    n_samples = params.shape[0]
     say("=" * 70)
     say("GENERATING SYNTHETIC HISTORICAL CALIBRATIONS (MI355X batch path)")
     say("=" * 70)
     say(f"  samples: {n_samples}   save path: {save_path}   COS terms: {N}")
     dates = trading_dates(n_samples)
-    params, spots, noise = draw_paths(n_samples)
-    model = price_grid(params, spots, N=N, device=device)
     market = model + noise * model                                   # (:141-142)
     rel = (model - market) / market
     losses = np.mean(rel ** 2, axis=1)                               # (:154-157)

@@ -1,0 +1,128 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of dhcos.distributed: the sharded multi-start and
+the sharded generator must return exactly what the single-process path returns.
+
+No GPU here, so the per-rank objective / pricer is the CPU oracle (test infrastructure, used as a
+stand-in for the device surface): what is under test is the sharding, the record exchange and the
+reference's best-start rule, not the kernels (those are covered by test_gpu_parity.py)."""
+import os
+import pickle
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dhcos import distributed as D
+from dhcos import generator as G
+from dhcos.calibrator import DoubleHestonJumpCalibrator
+from oracle import dh_oracle as O
+
+SPOT, R = 100.0, 0.05
+
+
+def _market():
+    prm = np.array([0.04, 2.0, 0.04, 0.3, -0.5, 0.04, 1.5, 0.04, 0.2, -0.3, 0.1, 0.0, 0.1])
+    out = []
+    for T in (0.25, 0.5, 1.0):
+        for K in (90.0, 95.0, 100.0, 105.0, 110.0):
+            out.append({"strike": K, "maturity": T, "option_type": "call",
+                        "price": float(O.price_vec(prm, SPOT, K, T, R, True, 64)) * 1.01})
+    return out
+
+
+class OracleCalibrator(DoubleHestonJumpCalibrator):
+    """The calibrator with its device surface replaced by the CPU oracle (N = 64)."""
+
+    def loss_batch(self, X, track=True):
+        X = np.atleast_2d(np.asarray(X, dtype=np.float64))
+        if track:
+            self.n_calls += X.shape[0]
+        return np.array([O.loss(x, self.market_options, self.spot, self.risk_free_rate, self.N)
+                         for x in X])
+
+    def _model_prices(self, params):
+        p = np.array([params[n] for n in self.param_names])
+        return np.array([O.price_vec(p, self.spot, o["strike"], o["maturity"],
+                                     self.risk_free_rate, True, self.N)
+                         for o in self.market_options])
+
+
+def oracle_price_fn(params, spots, N=64):
+    Krel = np.tile(G.STRIKES_PCT.astype(float), len(G.MATURITIES))
+    T = np.repeat(G.MATURITIES, len(G.STRIKES_PCT))
+    out = np.empty((params.shape[0], T.size))
+    for i in range(params.shape[0]):
+        K = Krel * spots[i] / 100.0
+        out[i] = [O.price_vec(params[i], spots[i], K[j], T[j], G.RISK_FREE, True, N)
+                  for j in range(T.size)]
+    return out
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir, n_starts, n_samples):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # only rank 0's RNG state matters: x0s and generator draws are broadcast from it
+        np.random.seed(0 if rank == 0 else 1234 + rank)
+        cal = OracleCalibrator(SPOT, R, _market(), N=64)
+        res = D.calibrate_sharded(cal, maxiter=2, multi_start=n_starts)
+        np.random.seed(7 if rank == 0 else 99)
+        gen = D.generate_sharded(n_samples, os.path.join(out_dir, f"gen{rank}.pkl"), N=64,
+                                 verbose=False, price_fn=oracle_price_fn)
+        with open(os.path.join(out_dir, f"rank{rank}.pkl"), "wb") as fh:
+            pickle.dump({"res": res, "gen": gen}, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,n_starts", [(2, 4), (3, 2)])
+def test_sharded_equals_single_process(tmp_path, world, n_starts):
+    n_samples = 5
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_starts, n_samples),
+             nprocs=world, join=True)
+    got = [pickle.load(open(tmp_path / f"rank{r}.pkl", "rb")) for r in range(world)]
+
+    np.random.seed(0)
+    cal = OracleCalibrator(SPOT, R, _market(), N=64)
+    want = cal.calibrate(maxiter=2, multi_start=n_starts)
+    for g in got:                       # every rank holds the same, reference-identical result
+        r = g["res"]
+        assert r.final_loss == want.final_loss
+        assert r.iterations == want.iterations
+        assert r.message == want.message
+        assert r.success == want.success
+        assert r.parameters == want.parameters
+        np.testing.assert_array_equal(r.model_prices, want.model_prices)
+
+    np.random.seed(7)
+    p, s, nz = G.draw_paths(n_samples)
+    ref = G.assemble(p, s, nz, oracle_price_fn(p, s), None, verbose=False)
+    gen = got[0]["gen"]
+    assert len(gen) == n_samples
+    for a, b in zip(gen, ref):
+        np.testing.assert_array_equal(a.market_prices, b.market_prices)
+        np.testing.assert_array_equal(a.model_prices, b.model_prices)
+        assert a.parameters == b.parameters and a.spot == b.spot and a.date == b.date
+        assert a.final_loss == b.final_loss
+    assert all(g["gen"] is None for g in got[1:])
+    # rank 0 saved the reference-format pickle; it names lbfgs_calibrator.CalibrationResult
+    raw = open(tmp_path / "gen0.pkl", "rb").read()
+    assert b"lbfgs_calibrator" in raw and b"CalibrationResult" in raw
+
+
+def test_shard_helpers():
+    assert D.start_shard(8, 1, 3) == [1, 4, 7]
+    assert sorted(sum((D.start_shard(64, r, 8) for r in range(8)), [])) == list(range(64))
+    blocks = [D.sample_block(10, r, 4) for r in range(4)]
+    assert blocks == [(0, 3), (3, 6), (6, 9), (9, 10)]
+    assert D.sample_block(2, 3, 4) == (2, 2)
+    s, out = D._decode(D._encode(5, None, 0.0))
+    assert s == 5 and out is None
