@@ -201,6 +201,14 @@ def main():
     prices_per_step = S * M
     value = prices_per_step * K_ * world / dt
 
+    # host-API rate (PCIe-inclusive: params H2D, losses D2H, synchronous) -- reported, not `value`
+    n_host = max(5, min(K_, 50))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n_host):
+        surf.loss_terms(host[i], N)
+    host_rate = prices_per_step * n_host / (time.perf_counter() - t0)
+
     # ---- roofline of the dominant op: one request = cos_table_kernel + cos_option_kernel ----
     reps = max(20, min(K_, 200))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -252,6 +260,7 @@ def main():
                  "seconds": tc, "starts": n_starts, "iterations": int(res.iterations),
                  "final_loss": float(res.final_loss), "message": res.message,
                  "lockstep_launches_rank0": int(getattr(c2, "lockstep_launches", 0)),
+                 "loss_evals_rank0": int(c2.loss_evals),
                  "calibrate": f"calibrate(maxiter=300, multi_start={n_starts}), np.random.seed(0)"
                               + (", starts sharded over ranks" if world > 1 else "")}
 
@@ -265,12 +274,18 @@ def main():
                        "param_sets_per_step": S, "prices_per_step": prices_per_step,
                        "parallelism": f"independent requests per rank x{world}"},
             "roofline": roofline,
+            "host_api_prices_per_sec": host_rate,
         }
         if calib:
             line["calibration"] = calib
         if not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(opts, S0, r, N, args.cpu_budget)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+            if calib and world == 1:
+                # the same calibration on the CPU port: every loss evaluation prices M options
+                cpu_s = calib["loss_evals_rank0"] * M / line["cpu_baseline"]["value"]
+                calib["cpu_port_seconds_extrapolated"] = cpu_s
+                calib["speedup_vs_cpu"] = cpu_s / calib["seconds"]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

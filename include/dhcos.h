@@ -66,7 +66,7 @@ void* dh_ctx_stream(dh_ctx* ctx);
  * operation order (own CF and sincos per COS term) instead of the shared-table fast path.   */
 int dh_ctx_set_exact(dh_ctx* ctx, int on);
 /* Diagnostics (only in the DH_STAMPS build, `make stamps`; the production library returns
- * DH_E_ARG): record per-block s_memtime phase stamps of the COS kernel, read the last launch's. */
+ * DH_E_ARG): record per-block s_memtime phase stamps of the COS kernels, read the last request's. */
 int dh_ctx_debug_stamps(dh_ctx* ctx, int on);
 int dh_ctx_read_stamps(dh_ctx* ctx, unsigned long long* out, int64_t cap, int64_t* n);
 
@@ -99,7 +99,8 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
 
 /* Device-pointer variants: params/out/sse/n_bad are device pointers; enqueue on `stream`
  * (hipStream_t; NULL = context stream).  No synchronisation, no allocation after warm-up.
- * dh_surface_loss_dev is ONE kernel launch (the last task of each param set finalises its sum).
+ * A request is two kernel launches (COS table, then options + fused loss: the last task of each
+ * param set finalises its sum in a fixed order).
  * Launches through one context share its scratch: issue them on one stream at a time.       */
 int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int64_t P,
                          int N, double L, double* d_out, void* stream);

@@ -118,6 +118,7 @@ class DoubleHestonJumpCalibrator:
         self.device = device
         self._surface = None
         self._surface_ok = None    # False when an option_type is '' (every loss is then 1e10)
+        self.loss_evals = 0        # param sets evaluated over the object's life (all starts)
 
     # ---- transforms (lbfgs_calibrator.py:62-116) ---------------------------------------
     def transform_params(self, x: np.ndarray) -> Dict[str, float]:
@@ -169,6 +170,7 @@ class DoubleHestonJumpCalibrator:
         """compute_loss for every row of X [S, 13] in one launch (reference semantics per row)."""
         X = np.atleast_2d(np.asarray(X, dtype=np.float64))
         S = X.shape[0]
+        self.loss_evals += S
         if track:
             self.n_calls += S
         M = len(self.market_options)
