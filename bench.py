@@ -119,7 +119,95 @@ CONFIGS = {
                         "starts x 14 param sets per step"),
     "c1": dict(nK=5, nT=3, N=128, starts=1, put_itm=False,
                workload="15-option grid (5 K x 3 T), N=128, one function+gradient request"),
+    "c5": dict(gen=True, P=1_000_000, N=128,
+               workload="generator batch: 1M param sets (synthetic_generator.py ranges) x 32 "
+                        "calls (8 K/S in linspace(0.8, 1.2) of each sample's spot x T in "
+                        "{0.25, 0.5, 1, 2}), N=128, priced in one pass per step"),
 }
+
+
+def bench_generator(args, cfg, world, rank, dev, coll, stream):
+    """C5: one step = price every (param set, option) of a 1M-sample generator batch
+    (dh_surface_price_dev, strikes K_relative * spot / 100 formed on the device)."""
+    sptr = stream.cuda_stream
+    P, N = cfg["P"], cfg["N"]
+    Krel = np.tile(np.linspace(80.0, 120.0, 8), 4)
+    T = np.repeat([0.25, 0.5, 1.0, 2.0], 8)
+    M = T.size
+    ctx = _native.default_context()
+    surf = _native.Surface(ctx, Krel, T, np.ones(M, dtype=np.int8),
+                           strike_mode=_native.STRIKE_PCT_SPOT)
+    rs = np.random.RandomState(5 + rank)
+    host = np.empty((P, 16))
+    host[:, :13] = GEN_LO + (GEN_HI - GEN_LO) * rs.rand(P, 13)
+    host[:, 13] = 100.0 * np.exp(np.cumsum(rs.normal(0.0003, 0.01, P)) * 0.01)  # spot walk
+    host[:, 14], host[:, 15] = 0.03, 0.0
+    d_params = torch.from_numpy(host).to(dev)
+    d_out = torch.empty((P, M), dtype=torch.float64, device=dev)
+
+    def run():
+        surf.price_dev(d_params.data_ptr(), P, d_out.data_ptr(), N=N, stream=sptr)
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    chk = np.arange(0, P, P // 64)
+    got = d_out[torch.from_numpy(chk).to(dev)].cpu().numpy()
+    assert np.array_equal(got, surf.price(host[chk], N)), "device/host path mismatch"
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([dt], dtype=torch.float64, device=coll)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    value = P * M * args.steps * world / dt
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(max(3, min(args.steps, 10)))]
+    for e0, e1 in evs:
+        e0.record(stream)
+        run()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    ker_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
+    G = 4
+    flop = P * G * N * FLOP_TAB + P * M * (N - 1) * FLOP_TERM + P * M * FLOP_OPT
+    alg_bytes = P * 16 * 8 + M * 17 + P * M * 8
+    roofline = {"bound": "valu_fp64", "achieved": round(flop / (ker_ms * 1e-3) / 1e12, 3),
+                "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(flop / (ker_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4),
+                "traffic": pmc_traffic(args.config),
+                "kernel": "cos_table_kernel + cos_option_kernel (all chunks of one batch, HIP events)",
+                "kernel_ms": round(ker_ms, 4), "flop_per_launch": flop,
+                "alg_bytes_per_launch": alg_bytes,
+                "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
+                        "peak_GBs": PEAK_HBM_GBS,
+                        "frac": alg_bytes / (ker_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}}
+    if rank == 0:
+        line = {"metric": "option-prices/sec (COS, generator batch)", "value": value,
+                "unit": "option-prices/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic",
+                "config": {"workload": cfg["workload"], "param_sets": P, "options": M,
+                           "cos_terms": N, "prices_per_step": P * M,
+                           "parallelism": f"independent batches per rank x{world}"},
+                "roofline": roofline}
+        if not args.no_cpu:
+            opts = [{"strike": float(k), "maturity": float(t), "option_type": "call", "price": 1.0}
+                    for k, t in zip(Krel, T)]
+            line["cpu_baseline"] = cpu_baseline(opts, 100.0, 0.03, N, args.cpu_budget)
+            line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -155,6 +243,8 @@ def main():
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     assert sptr, "expected a non-default HIP stream"
+    if cfg.get("gen"):
+        return bench_generator(args, cfg, world, rank, dev, coll, stream)
 
     opts, S0, r = make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
     M = len(opts)

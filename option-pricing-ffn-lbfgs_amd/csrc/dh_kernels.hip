@@ -16,8 +16,13 @@
 //       th = pi (log(K/S0) - a)/(b - a),   price = e^{-rT} (const + w0 V_0 - e^{xK} S2 + K S4)
 //     computed by G lanes per group of kR options (lane j: k = 1 + j, 1 + j + G, ...), the
 //     angle advanced by complex rotations e^{i G th} with an exact sincos re-anchor every
-//     kAnchor steps, then DPP butterflies.  Options whose [a, b] is widened by the log-strike
-//     clamp (double_heston.py:135-137) are priced inline by a per-term path on their own range.
+//     kAnchor steps, then DPP butterflies.
+//
+//   Options whose [a, b] is widened by the log-strike clamp (double_heston.py:135-137) are
+//   found and priced by the TABLE kernel (it already carries the CF code): per (p, group) it
+//   writes a 64-bit mask word per 64 options and the clamped options' prices (per-term path on
+//   the option's own range).  The option kernel only reads them, so it carries no CF code and
+//   runs at ~100 VGPRs (4-5 waves per SIMD) instead of ~200.
 //     Loss mode: fixed-order per-task partial of sum rel^2 and #invalid; the last task of p to
 //     finish (agent-scope counter, sc1 hand-off) sums the partials in tile order.  No float
 //     atomics: bitwise reproducible, independent of how many param sets share the launch.
@@ -59,6 +64,8 @@ struct PriceArgs {
     const double* mkt;      // [M] or null
     const int* perm;        // [M] sorted -> caller index
     const int2* tiles;      // [n_tiles] (opt0, nopt)
+    const int2* groups;     // [n_groups] (opt0, nopt) of each maturity group (null if paired)
+    int max_group;          // largest group (clamp price slots per table)
     const int* tile_group;  // [n_tiles] maturity group of each tile
     const double* group_T;  // [n_groups]
     int n_tiles, n_groups;
@@ -78,6 +85,8 @@ struct PriceArgs {
     int* n_bad;             // [P]
     double* table;          // workspace: [np*tabs_per_p][N] = w_k
     double* consts;         // workspace: [np*tabs_per_p][kConsts]
+    unsigned long long* cl_mask;   // workspace: [np*tabs_per_p][cl_words] clamp bits per option
+    double* cl_price;       // workspace: [np*tabs_per_p][max_group] prices of clamped options
     unsigned long long* stamps;   // diagnostic builds (DH_STAMPS) only: [blocks][kStamps]
 };
 
@@ -98,6 +107,13 @@ constexpr int kStamps = 8;
 #endif
 
 __host__ __device__ inline int tabs_per_p(const PriceArgs& A) { return A.paired ? 1 : A.n_groups; }
+__host__ __device__ inline int cl_words(const PriceArgs& A) { return (A.max_group + 63) / 64; }
+
+// log(K / S0) and K / S0 (= e^{xK} to an ulp) of sorted option m under spot S0
+__device__ __forceinline__ double option_logk(double K, double S0, double& ratio) {
+    ratio = K / S0;
+    return dh::dlog(ratio);                                          // double_heston.py:162
+}
 
 __device__ __forceinline__ double option_strike(const PriceArgs& A, int m, double S0) {
     const double Kin = A.K[m];
@@ -107,6 +123,28 @@ __device__ __forceinline__ double option_strike(const PriceArgs& A, int m, doubl
 // ----------------------------------------------------------------------------------------------
 // table kernel
 // ----------------------------------------------------------------------------------------------
+// Per-term path for a clamp-widened option: own range [a, b], own u grid, CF per term (fast
+// exponent form) and the generic chi/psi (double_heston.py:141-158,160-192).  Lane share of
+// the sum' over k = k_first, k_first + k_step, ...
+__device__ __forceinline__ double clamped_term_sum(const Params& P, double T, double K, double xK,
+                                                   double a, double b, bool is_call, int k_first,
+                                                   int k_step, int N) {
+    const dh::CfConsts CC = dh::cf_consts(P, T);
+    const double ba = b - a;
+    const double scale = 2.0 / ba;
+    double acc = 0.0;
+    for (int k = k_first; k < N; k += k_step) {
+        const double u = k * dh::kPi / ba;
+        const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+        double chi, psi;
+        if (is_call) dh::cos_coeffs(k, xK, b, a, b, chi, psi);
+        else dh::cos_coeffs(k, a, xK, a, b, chi, psi);
+        const double V = is_call ? (P.S0 * chi - K * psi) : (K * psi - P.S0 * chi);
+        acc += (k == 0 ? 0.5 : 1.0) * w * V;
+    }
+    return acc;
+}
+
 // per-table constants broadcast through LDS (computed by the first wave of the table)
 constexpr int kTabC = 6 + 16;   // a, b, e^b, e^a, 2/(b-a), pi/(b-a) | CfConsts (16 doubles)
 static_assert(sizeof(dh::CfConsts) == 16 * sizeof(double), "CfConsts layout");
@@ -213,6 +251,47 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
         cs[6] = eb;
         cs[7] = ea;
     }
+
+    // ---- clamp-widened options of this table's group (double_heston.py:135-137) ----
+    // 64 options per wave step: a ballot of the clamp test, then the wave prices each clamped
+    // option on its own range [min(a, xK - 0.1), max(b, xK + 0.1)] (lanes over k).  The mask
+    // words are written for every option; prices only for clamped ones.  The option kernel
+    // trusts these bits, so the two kernels can never disagree on the decision.
+    if (active) {
+        int g0 = (int)p, gn = 1;
+        if (!A.paired) {
+            const int2 gr = A.groups[g];
+            g0 = gr.x;
+            gn = gr.y;
+        }
+        const double disc = exp(-P.r * T);
+        const int64_t slot0 = q * (int64_t)A.max_group;
+        for (int base = wv * 64; base < gn; base += kWaves * 64) {
+            const int i = base + lane;
+            bool cl = false;
+            double xK = 0.0, K = 0.0;
+            if (i < gn) {
+                K = option_strike(A, g0 + i, P.S0);
+                double ratio;
+                xK = option_logk(K, P.S0, ratio);
+                cl = xK - 0.1 < a || xK + 0.1 > b;
+            }
+            unsigned long long mask = __ballot(cl);
+            if (lane == 0) A.cl_mask[q * cl_words(A) + base / 64] = mask;
+            while (mask) {
+                const int l = __ffsll((long long)mask) - 1;
+                mask &= mask - 1;
+                const double x = __shfl(xK, l, 64);
+                const double Kl = __shfl(K, l, 64);
+                const int m = g0 + base + l;
+                const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
+                const double bc = (x + 0.1 > b) ? x + 0.1 : b;
+                double v = clamped_term_sum(P, T, Kl, x, ac, bc, A.call[m] != 0, lane, 64, N);
+                for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+                if (lane == 0) A.cl_price[slot0 + base + l] = disc * v;
+            }
+        }
+    }
     DH_STAMP(A, 7);
 }
 
@@ -275,28 +354,6 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
     }
 }
 
-// Per-term path for a clamp-widened option: own range [a, b], own u grid, CF per term (fast
-// exponent form) and the generic chi/psi (double_heston.py:141-158,160-192).  Lane share of
-// the sum' over k = k_first, k_first + k_step, ...
-__device__ __forceinline__ double clamped_term_sum(const Params& P, double T, double K, double xK,
-                                                   double a, double b, bool is_call, int k_first,
-                                                   int k_step, int N) {
-    const dh::CfConsts CC = dh::cf_consts(P, T);
-    const double ba = b - a;
-    const double scale = 2.0 / ba;
-    double acc = 0.0;
-    for (int k = k_first; k < N; k += k_step) {
-        const double u = k * dh::kPi / ba;
-        const double w = dh::cf_phase_re(CC, u, T, a) * scale;
-        double chi, psi;
-        if (is_call) dh::cos_coeffs(k, xK, b, a, b, chi, psi);
-        else dh::cos_coeffs(k, a, xK, a, b, chi, psi);
-        const double V = is_call ? (P.S0 * chi - K * psi) : (K * psi - P.S0 * chi);
-        acc += (k == 0 ? 0.5 : 1.0) * w * V;
-    }
-    return acc;
-}
-
 __device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int col, double mk,
                                              int oi, double price, double* lsse, double* lbad) {
     if (A.out) A.out[p * A.out_stride + col] = price;
@@ -352,8 +409,8 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
 
 __host__ __device__ constexpr int option_lds_doubles(int N, int opt_cap) {
     // (T2,T3)[N] T4[N] u[N] | K, mkt, sse, bad, xK, e^xK, cos/sin step [opt_cap] |
-    // call, perm, clamp [opt_cap] ints + clamp count, rounded to whole 16-byte pairs
-    return 4 * N + 8 * opt_cap + ((3 * opt_cap + 1 + 3) / 4) * 2;
+    // call, perm [opt_cap] ints, rounded to whole 16-byte pairs
+    return 4 * N + 8 * opt_cap + ((2 * opt_cap + 3) / 4) * 2;
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -390,8 +447,6 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     double* lss = lcs + cap;
     int* lcall = (int*)(lss + cap);
     int* lperm = lcall + cap;
-    int* lclamp = lperm + cap;                         // [cap] clamped option indices
-    int* ncl = lclamp + cap;                           // [1] count
 
     int opt0 = 0, nopt = 0, g = 0;
     if (active) {
@@ -420,10 +475,11 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
         C = Consts{cs[0], cs[1], cs[2], cs[3], cs[4], cs[5], cs[6], cs[7]};
     }
     const double ba = C.b - C.a;
-    if (t == 0) *ncl = 0;
+    const double T = active ? A.T[opt0] : 1.0;
+    const double disc = exp(-P.r * T);
     // stage the (p, g) table, expanded to u, (T2, T3), T4 (same expressions as the table
-    // kernel's k-sums), and per-option data: log(K/S0), e^{xK}, the clamp test
-    // (double_heston.py:135-137) and the G-step rotation of each option
+    // kernel's k-sums), and per-option data: log(K/S0), e^{xK} and the G-step rotation of each
+    // option; clamp-widened options (bit set by the table kernel) are recorded right here
     if (active) {
         const double* tw = A.table + q * (int64_t)N;
         const double piba = dh::kPi / ba;
@@ -435,28 +491,29 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
             t4[k] = k == 0 ? 0.0 : w * dh::drcp(u);
             tu[k] = u;
         }
-        const bool pct = A.strike_mode == DH_STRIKE_PCT_SPOT;
         const double ustep = G * dh::kPi / ba;
+        const int g0 = A.paired ? (int)p : A.groups[g].x;
+        const unsigned long long* msk = A.cl_mask + q * cl_words(A);
+        const double* clp = A.cl_price + q * (int64_t)A.max_group;
         for (int i = t; i < nopt; i += TPT) {
-            const double Kin = A.K[opt0 + i];
-            const double K = pct ? Kin * P.S0 / 100.0 : Kin;
-            const double ratio = K / P.S0;
-            const double xK = dh::dlog(ratio);                       // double_heston.py:162
+            const double K = option_strike(A, opt0 + i, P.S0);
+            double ratio;
+            const double xK = option_logk(K, P.S0, ratio);
             lK[i] = K;
             lmkt[i] = A.mkt ? A.mkt[opt0 + i] : 0.0;
             lcall[i] = A.call[opt0 + i];
             lperm[i] = A.perm[opt0 + i];
             lxK[i] = xK;
             lexK[i] = ratio;                                         // e^{xK} to an ulp
-            const bool cl = xK - 0.1 < C.a || xK + 0.1 > C.b;
+            const int gpos = opt0 + i - g0;
+            const bool cl = (msk[gpos >> 6] >> (gpos & 63)) & 1ull;
             double ss, cs;
             dh::dsincos(ustep * (cl ? 0.0 : xK - C.a), &ss, &cs);
             lcs[i] = cs;
             lss[i] = cl ? NAN : ss;                                  // NaN marks clamped
+            if (cl) record_price(A, p, lperm[i], lmkt[i], i, clp[gpos], lsse, lbad);
         }
     }
-    const double T = active ? A.T[opt0] : 1.0;
-    const double disc = exp(-P.r * T);
     __syncthreads();
     DH_STAMP(A, 1);
 
@@ -472,9 +529,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
             const int oi = gi * R + j;
             const bool in = gvalid && j < R && oi < nopt;
             const double sj = in ? lss[oi] : 0.0;
-            const bool clamped = in && isnan(sj);
-            if (clamped && gl == 0) lclamp[atomicAdd(ncl, 1)] = oi;   // priced below
-            use[j] = in && !clamped;
+            use[j] = in && !isnan(sj);                               // clamped: recorded
             dx[j] = use[j] ? lxK[oi] - C.a : 0.0;
             cs[j] = use[j] ? lcs[oi] : 1.0;
             ss[j] = use[j] ? sj : 0.0;
@@ -514,19 +569,6 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
                 record_price(A, p, lperm[oi], lmkt[oi], oi, disc * sum, lsse, lbad);
             }
         }
-    }
-    // clamp-widened options (double_heston.py:135-137): per-term path on each option's own
-    // range, one wave per option (no barrier inside: trip counts may differ between tasks)
-    __syncthreads();
-    const int n_cl = active ? *ncl : 0;
-    for (int c = t >> 6; c < n_cl; c += TPT / 64) {
-        const int oi = lclamp[c];
-        const double x = lxK[oi];
-        const double a = (x - 0.1 < C.a) ? x - 0.1 : C.a;      // Python min/max
-        const double b = (x + 0.1 > C.b) ? x + 0.1 : C.b;
-        double v = clamped_term_sum(P, T, lK[oi], x, a, b, lcall[oi] != 0, t & 63, 64, N);
-        for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
-        if ((t & 63) == 0) record_price(A, p, lperm[oi], lmkt[oi], oi, disc * v, lsse, lbad);
     }
     DH_STAMP(A, 2);
 
@@ -703,8 +745,8 @@ int option_tpt(int max_nopt, int N, int cap) {
 struct dh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, aux0,
-        aux1, aux2, aux3;
+    DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, cl_mask,
+        cl_price, aux0, aux1, aux2, aux3;
     bool attr_set = false;
     int exact = 0;          // validation mode: every option through the per-term exact path
     int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
@@ -718,6 +760,7 @@ struct dh_surface {
     int n_tiles = 0;
     int n_groups = 0;       // distinct maturities
     int max_nopt = 0;       // largest tile
+    int max_group = 0;      // largest maturity group
     int strike_mode = 0;
     bool has_mkt = false;
     double* K = nullptr;
@@ -728,6 +771,7 @@ struct dh_surface {
     int2* tiles = nullptr;
     int* tile_group = nullptr;
     double* group_T = nullptr;
+    int2* groups = nullptr;
 };
 
 namespace {
@@ -787,10 +831,14 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     if (rc) return rc;
     const int N = A0.N;
     const int tpp = A0.paired ? 1 : A0.n_groups;
-    const size_t per_p = (size_t)tpp * ((size_t)N + kConsts) * sizeof(double);
+    const int words = cl_words(A0);
+    const size_t per_p =
+        (size_t)tpp * ((size_t)N + kConsts + words + (size_t)A0.max_group) * sizeof(double);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A0.P, kTableBudget / per_p));
     HIP_TRY(ctx->table.reserve((size_t)chunk * tpp * N * sizeof(double)));
     HIP_TRY(ctx->consts.reserve((size_t)chunk * tpp * kConsts * sizeof(double)));
+    HIP_TRY(ctx->cl_mask.reserve((size_t)chunk * tpp * words * 8));
+    HIP_TRY(ctx->cl_price.reserve((size_t)chunk * tpp * A0.max_group * sizeof(double)));
     const int t1 = table_tpt(N);
     const int max_nopt = A0.paired ? 1 : A0.opt_cap;
     const int t2 = option_tpt(max_nopt, N, A0.opt_cap);
@@ -809,6 +857,8 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         A.np = std::min<int64_t>(chunk, A0.P - p0);
         A.table = (double*)ctx->table.ptr;
         A.consts = (double*)ctx->consts.ptr;
+        A.cl_mask = (unsigned long long*)ctx->cl_mask.ptr;
+        A.cl_price = (double*)ctx->cl_price.ptr;
         A.stamps = ctx->stamps_on ? (unsigned long long*)ctx->stamps.ptr : nullptr;
         const int64_t n_q = A.np * tpp;
         const int64_t b1 = (n_q + kBlock / t1 - 1) / (kBlock / t1);
@@ -883,7 +933,7 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->params, &ctx->out, &ctx->sse, &ctx->bad, &ctx->part_sse,
                       &ctx->part_bad, &ctx->counter, &ctx->exact_prices, &ctx->stamps, &ctx->table,
-                      &ctx->consts, &ctx->aux0,
+                      &ctx->consts, &ctx->cl_mask, &ctx->cl_price, &ctx->aux0,
                       &ctx->aux1, &ctx->aux2, &ctx->aux3})
         b->release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -954,10 +1004,13 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
     std::vector<int2> tiles;
     std::vector<int> tile_group;
     std::vector<double> group_T;
-    int max_nopt = 0;
+    std::vector<int2> groups;
+    int max_nopt = 0, max_group = 0;
     for (int i = 0; i < M;) {
         int j = i;
         while (j < M && sT[j] == sT[i]) ++j;
+        groups.push_back(make_int2(i, j - i));
+        max_group = std::max(max_group, j - i);
         for (int s = i; s < j; s += kTileMax) {
             tiles.push_back(make_int2(s, std::min(kTileMax, j - s)));
             tile_group.push_back((int)group_T.size());
@@ -973,6 +1026,7 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
     s->n_tiles = (int)tiles.size();
     s->n_groups = (int)group_T.size();
     s->max_nopt = max_nopt;
+    s->max_group = max_group;
     s->strike_mode = strike_mode;
     s->has_mkt = mkt != nullptr;
     const size_t m8 = std::max<size_t>(1, (size_t)M) * 8;
@@ -988,6 +1042,7 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
     alloc((void**)&s->tiles, std::max<size_t>(1, tiles.size()) * sizeof(int2));
     alloc((void**)&s->tile_group, std::max<size_t>(1, tile_group.size()) * sizeof(int));
     alloc((void**)&s->group_T, std::max<size_t>(1, group_T.size()) * sizeof(double));
+    alloc((void**)&s->groups, std::max<size_t>(1, groups.size()) * sizeof(int2));
     if (e == hipSuccess && M > 0) {
         e = hipMemcpy(s->K, sK.data(), (size_t)M * 8, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(s->T, sT.data(), (size_t)M * 8, hipMemcpyHostToDevice);
@@ -1003,6 +1058,9 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
         if (e == hipSuccess)
             e = hipMemcpy(s->group_T, group_T.data(), group_T.size() * sizeof(double),
                           hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(s->groups, groups.data(), groups.size() * sizeof(int2),
+                          hipMemcpyHostToDevice);
     }
     if (e != hipSuccess) {
         dh_surface_destroy(s);
@@ -1016,7 +1074,7 @@ int dh_surface_destroy(dh_surface* s) {
     if (!s) return DH_OK;
     if (s->ctx) (void)hipSetDevice(s->ctx->device);
     for (void* p : {(void*)s->K, (void*)s->T, (void*)s->mkt, (void*)s->call, (void*)s->perm,
-                    (void*)s->tiles, (void*)s->tile_group, (void*)s->group_T})
+                    (void*)s->tiles, (void*)s->tile_group, (void*)s->group_T, (void*)s->groups})
         if (p) (void)hipFree(p);
     delete s;
     return DH_OK;
@@ -1042,6 +1100,8 @@ static PriceArgs surface_args(const dh_surface* s, const double* d_params, int64
     A.tiles = s->tiles;
     A.tile_group = s->tile_group;
     A.group_T = s->group_T;
+    A.groups = s->groups;
+    A.max_group = s->max_group;
     A.n_tiles = s->n_tiles;
     A.n_groups = s->n_groups;
     A.opt_cap = ((s->max_nopt + 1) / 2) * 2;
@@ -1192,6 +1252,7 @@ int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const dou
     A.perm = (const int*)ctx->aux3.ptr;
     A.paired = 1;
     A.opt_cap = 2;
+    A.max_group = 1;
     A.M = (int)P;
     A.exact = ctx->exact;
     A.strike_mode = DH_STRIKE_ABSOLUTE;

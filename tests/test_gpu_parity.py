@@ -351,3 +351,49 @@ def test_fast_path_matches_exact_mode_full_size(dh):
     finally:
         ctx.set_exact(False)
     assert rel_close(fast, exact, 1e-11, 1e-11).all(), np.max(np.abs(fast - exact))
+
+
+def test_clamped_options_across_mask_words_and_tiles(dh):
+    """The table kernel decides and prices clamp-widened options (double_heston.py:135-137) and
+    the option kernel looks them up by a per-(p, group) bit mask.  One maturity group of 300
+    options = 2 tiles and 5 mask words; clamped strikes sit in several words and both tiles;
+    price mode, loss mode and paired mode against the oracle and the exact kernel."""
+    from dhcos import _native
+    rs = np.random.RandomState(21)
+    M, P, N = 300, 5, 128
+    lo = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
+    hi = np.array([0.08, 4.5, 0.065, 0.5, -0.4, 0.07, 1.2, 0.07, 0.35, -0.2, 0.25, -0.01, 0.12])
+    params = lo + (hi - lo) * rs.rand(P, 13)
+    rec = np.zeros((P, 16))
+    rec[:, :13], rec[:, 13], rec[:, 14] = params, 100.0, 0.03
+    K = 100.0 * rs.uniform(0.85, 1.15, M)
+    far = [3, 64, 65, 130, 200, 255, 256, 299]              # words 0..4, tile 0 and tile 1
+    K[far] = [4.0, 9.0, 2500.0, 6.0, 800.0, 3.0, 1200.0, 7.5]
+    T = np.full(M, 0.08)
+    call = rs.rand(M) < 0.5
+    ctx = _native.default_context()
+    mkt = O.price_many(params[0], 100.0, K, T, 0.03, call, N)
+    want = np.stack([O.price_many(params[p], 100.0, K, T, 0.03, call, N) for p in range(P)])
+    # the reference's clamp is active on the far strikes only (checked on the oracle's ranges)
+    a, b = O.trunc_range(params[0], 100.0, 100.0, 0.08, 0.03)    # ATM: the unclamped range
+    xf = np.log(K[far] / 100.0)
+    assert np.all((xf - 0.1 < a) | (xf + 0.1 > b))
+    xn = np.log(np.delete(K, far) / 100.0)
+    assert np.all((xn - 0.1 > a) & (xn + 0.1 < b))
+    surf = _native.Surface(ctx, K, T, call, np.abs(mkt) + 1e-3)
+    got = surf.price(rec, N)
+    assert rel_close(got, want, FID_RTOL, BAR_ATOL).all(), np.max(np.abs(got - want))
+    sse, bad, prices = surf.loss_terms(rec, N, want_prices=True)
+    assert np.array_equal(prices, got)
+    m = np.abs(mkt) + 1e-3
+    ref_sse = np.sum(((got - m) / m) ** 2, axis=1)
+    assert rel_close(sse, ref_sse, 1e-12, 0).all()
+    assert np.array_equal(bad, np.sum(~(got > 0) | ~np.isfinite(got), axis=1))
+    ctx.set_exact(True)
+    try:
+        exact = surf.price(rec, N)
+    finally:
+        ctx.set_exact(False)
+    assert rel_close(got, exact, 1e-11, 1e-11).all(), np.max(np.abs(got - exact))
+    pairs = ctx.price_pairs(np.repeat(rec[:1], len(far), 0), K[far], T[far], call[far], N)
+    assert rel_close(pairs, want[0, far], FID_RTOL, BAR_ATOL).all()
