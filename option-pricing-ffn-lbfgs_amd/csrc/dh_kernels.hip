@@ -3,6 +3,8 @@
 // Two kernels per request (DESIGN.md "Kernels"), each with its own small register footprint:
 //
 //   cos_table_kernel<TPT>  one table per (param set p, maturity group g):  for k < N
+//     (blocks = resident capacity, each a contiguous range of tables; prologues of up to 64
+//     tables computed lane-parallel by one wave)
 //       w_k = Re(phi(u_k) e^{-i u_k a}) 2/(b-a)            (double_heston.py:48-97,163-168,187)
 //     (8 bytes per term) plus per-(p, g) constants c0/c1 (call), c5 (put), w0 (k = 0 weight),
 //     a, b, e^b, e^a reduced in a fixed order.  CF-bound; the table lands in an L2/MALL-resident
@@ -145,44 +147,60 @@ __device__ __forceinline__ double clamped_term_sum(const Params& P, double T, do
     return acc;
 }
 
-// per-table constants broadcast through LDS (computed by the first wave of the table)
-constexpr int kTabC = 6 + 16;   // a, b, e^b, e^a, 2/(b-a), pi/(b-a) | CfConsts (16 doubles)
+// per-table values staged in LDS by the prologue lane of the table:
+//   [0..5] a, b, e^b, e^a, 2/(b-a), pi/(b-a) | [6..21] CfConsts | [22] S0, [23] r, [24] T,
+//   [25] K/S0 below which the clamp test must be evaluated, [26] above which (prefilter),
+//   [27] group's first option, [28] group size (as doubles)
+constexpr int kTabC = 29;
+constexpr double kClampMargin = 1e-9;   // relative safety margin of the K-space prefilter
 static_assert(sizeof(dh::CfConsts) == 16 * sizeof(double), "CfConsts layout");
 
 #ifndef DH_TABLE_WAVES
-#define DH_TABLE_WAVES 1    // occupancy hint (min waves per SIMD) for the register allocator
+#define DH_TABLE_WAVES 2    // min waves per SIMD: caps VGPR+AGPR at 256 (the CF needs ~250)
 #endif
 #ifndef DH_OPTION_WAVES
 #define DH_OPTION_WAVES 1
 #endif
 
+// Grid: a fixed number of blocks (resident capacity), each owning a contiguous range of tables.
+// Tables are taken in batches of up to kBatch: lane i of wave 0 computes the truncation range and
+// CF constants of table i of the batch (one prologue latency for up to 64 tables), then every
+// table slot (TPT threads) runs the CF loops of its tables back to back; per-table sums are
+// finished in a fixed order at the end of the batch (bitwise independent of the grid).
+constexpr int kBatch = 64;
+
 template <int TPT>
 __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(PriceArgs A) {
-    constexpr int kTabs = kBlock / TPT;
-    constexpr int kWaves = TPT / 64;
-    __shared__ double red[kTabs][4][kWaves];
-    __shared__ double shc[kTabs][kTabC];
-    const int slot = threadIdx.x / TPT;
+    constexpr int kTabs = kBlock / TPT;      // table slots per block
+    constexpr int kWaves = TPT / 64;         // waves per slot
+    __shared__ double shc[kBatch][kTabC];
+    __shared__ double red[kBatch][4][kWaves];
+    const int slot = __builtin_amdgcn_readfirstlane(threadIdx.x / TPT);
     const int t = threadIdx.x % TPT;
     const int lane = threadIdx.x & 63;
     const int wv = t >> 6;
     const int N = A.N;
     const int tpp = tabs_per_p(A);
     const int64_t n_q = A.np * tpp;
-    const int64_t q = (int64_t)blockIdx.x * kTabs + __builtin_amdgcn_readfirstlane(slot);
-    const bool active = q < n_q;
-    const int64_t p = A.p0 + (active ? q / tpp : 0);
-    const int g = active ? (int)(q % tpp) : 0;
-    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
-    const double T = !active ? 1.0 : (A.paired ? A.T[p] : A.group_T[g]);
+    const int64_t q_begin = n_q * blockIdx.x / gridDim.x;
+    const int64_t q_end = n_q * (blockIdx.x + 1) / gridDim.x;
     DH_STAMP(A, 4);
 
-    if (wv == 0) {   // truncation range and CF constants once per table
-        double a, b;
-        dh::trunc_unclamped(P, T, A.L, a, b);            // double_heston.py:100-132
-        const dh::CfConsts CC = dh::cf_consts(P, T);
-        if (lane == 0) {
-            double* c = shc[slot];
+    for (int64_t b0 = q_begin; b0 < q_end; b0 += kBatch) {
+        const int nb = (int)min<int64_t>(kBatch, q_end - b0);
+        // ---- prologue, one lane per table: truncation range and CF constants ----
+        if (threadIdx.x < nb) {
+            const int64_t q = b0 + threadIdx.x;
+            const int64_t p = A.p0 + q / tpp;
+            const int g = (int)(q % tpp);
+            const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
+            const double T = A.paired ? A.T[p] : A.group_T[g];
+            int2 gr = make_int2((int)p, 1);
+            if (!A.paired) gr = A.groups[g];
+            double a, b;
+            dh::trunc_unclamped(P, T, A.L, a, b);            // double_heston.py:100-132
+            const dh::CfConsts CC = dh::cf_consts(P, T);
+            double* c = shc[threadIdx.x];
             c[0] = a;
             c[1] = b;
             c[2] = exp(b);
@@ -191,106 +209,124 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             c[5] = dh::kPi / (b - a);
             const double* cc = (const double*)&CC;
             for (int i = 0; i < 16; ++i) c[6 + i] = cc[i];
+            c[22] = P.S0;
+            c[23] = P.r;
+            c[24] = T;
+            // unclamped iff a + 0.1 <= log(K/S0) <= b - 0.1: strikes whose K/S0 is inside these
+            // bounds by a 1e-9 relative margin cannot be clamped (exp/log errors are ~1e-16)
+            c[25] = exp(a + 0.1) * (1.0 + kClampMargin);
+            c[26] = exp(b - 0.1) * (1.0 - kClampMargin);
+            c[27] = gr.x;
+            c[28] = gr.y;
         }
-    }
-    __syncthreads();
-    DH_STAMP(A, 5);
-    const double* c = shc[slot];
-    const double a = c[0], b = c[1], eb = c[2], ea = c[3], scale = c[4], piba = c[5];
-    dh::CfConsts CC;
-    {
-        double* cc = (double*)&CC;
-        for (int i = 0; i < 16; ++i) cc[i] = c[6 + i];
-    }
-    const double ba = b - a;
-    double* tw = A.table + (active ? q : 0) * (int64_t)N;
-    double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
-    if (active) {
-        for (int k = t; k < N; k += TPT) {
-            const double u = k * piba;                       // k pi / (b - a)
-            const double w = dh::cf_phase_re(CC, u, T, a) * scale;
-            tw[k] = w;
-            if (k == 0) {
-                w0 = 0.5 * w;
-                continue;
-            }
-            double sb, cb;
-            dh::dsincos(u * ba, &sb, &cb);
-            const double T2 = w * P.S0 * dh::drcp(1.0 + u * u);
-            const double T4 = w * dh::drcp(u);
-            c0 += T2 * eb * (cb + u * sb);
-            c1 += T4 * sb;
-            c5 += T2 * ea;
-        }
-    }
-    DH_STAMP(A, 6);
-    for (int off = 1; off < 64; off <<= 1) {
-        c0 += __shfl_xor(c0, off, 64);
-        c1 += __shfl_xor(c1, off, 64);
-        c5 += __shfl_xor(c5, off, 64);
-        w0 += __shfl_xor(w0, off, 64);
-    }
-    if (lane == 0) {
-        red[slot][0][wv] = c0;
-        red[slot][1][wv] = c1;
-        red[slot][2][wv] = c5;
-        red[slot][3][wv] = w0;
-    }
-    __syncthreads();
-    if (active && t == 0) {
-        double sm[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int j = 0; j < 4; ++j)
-            for (int i = 0; i < kWaves; ++i) sm[j] += red[slot][j][i];
-        double* cs = A.consts + q * kConsts;
-        cs[0] = sm[0];
-        cs[1] = sm[1];
-        cs[2] = sm[2];
-        cs[3] = sm[3];
-        cs[4] = a;
-        cs[5] = b;
-        cs[6] = eb;
-        cs[7] = ea;
-    }
+        __syncthreads();
+        if (b0 == q_begin) DH_STAMP(A, 5);
 
-    // ---- clamp-widened options of this table's group (double_heston.py:135-137) ----
-    // 64 options per wave step: a ballot of the clamp test, then the wave prices each clamped
-    // option on its own range [min(a, xK - 0.1), max(b, xK + 0.1)] (lanes over k).  The mask
-    // words are written for every option; prices only for clamped ones.  The option kernel
-    // trusts these bits, so the two kernels can never disagree on the decision.
-    if (active) {
-        int g0 = (int)p, gn = 1;
-        if (!A.paired) {
-            const int2 gr = A.groups[g];
-            g0 = gr.x;
-            gn = gr.y;
-        }
-        const double disc = exp(-P.r * T);
-        const int64_t slot0 = q * (int64_t)A.max_group;
-        for (int base = wv * 64; base < gn; base += kWaves * 64) {
-            const int i = base + lane;
-            bool cl = false;
-            double xK = 0.0, K = 0.0;
-            if (i < gn) {
-                K = option_strike(A, g0 + i, P.S0);
-                double ratio;
-                xK = option_logk(K, P.S0, ratio);
-                cl = xK - 0.1 < a || xK + 0.1 > b;
+        for (int i = slot; i < nb; i += kTabs) {
+            const int64_t q = b0 + i;
+            const double* c = shc[i];
+            const double a = c[0], b = c[1], eb = c[2], ea = c[3], scale = c[4], piba = c[5];
+            dh::CfConsts CC;
+            {
+                double* cc = (double*)&CC;
+                for (int j = 0; j < 16; ++j) cc[j] = c[6 + j];
             }
-            unsigned long long mask = __ballot(cl);
-            if (lane == 0) A.cl_mask[q * cl_words(A) + base / 64] = mask;
-            while (mask) {
-                const int l = __ffsll((long long)mask) - 1;
-                mask &= mask - 1;
-                const double x = __shfl(xK, l, 64);
-                const double Kl = __shfl(K, l, 64);
-                const int m = g0 + base + l;
-                const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
-                const double bc = (x + 0.1 > b) ? x + 0.1 : b;
-                double v = clamped_term_sum(P, T, Kl, x, ac, bc, A.call[m] != 0, lane, 64, N);
-                for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
-                if (lane == 0) A.cl_price[slot0 + base + l] = disc * v;
+            const double S0 = c[22], T = c[24], lo = c[25], hi = c[26];
+            const int g0 = (int)c[27], gn = (int)c[28];
+            // strike of this lane's first clamp-scan option, loaded now, used after the CF loop
+            const int o_first = wv * 64 + lane;
+            const double K_first = o_first < gn ? option_strike(A, g0 + o_first, S0) : 0.0;
+            const double ba = b - a;
+            double* tw = A.table + q * (int64_t)N;
+            double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
+            for (int k = t; k < N; k += TPT) {
+                const double u = k * piba;                       // k pi / (b - a)
+                const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+                tw[k] = w;
+                if (k == 0) {
+                    w0 = 0.5 * w;
+                    continue;
+                }
+                double sb, cb;
+                dh::dsincos(u * ba, &sb, &cb);
+                const double T2 = w * S0 * dh::drcp(1.0 + u * u);
+                const double T4 = w * dh::drcp(u);
+                c0 += T2 * eb * (cb + u * sb);
+                c1 += T4 * sb;
+                c5 += T2 * ea;
+            }
+            for (int off = 1; off < 64; off <<= 1) {
+                c0 += __shfl_xor(c0, off, 64);
+                c1 += __shfl_xor(c1, off, 64);
+                c5 += __shfl_xor(c5, off, 64);
+                w0 += __shfl_xor(w0, off, 64);
+            }
+            if (lane == 0) {
+                red[i][0][wv] = c0;
+                red[i][1][wv] = c1;
+                red[i][2][wv] = c5;
+                red[i][3][wv] = w0;
+            }
+
+            // ---- clamp-widened options of this table's group (double_heston.py:135-137) ----
+            // 64 options per wave step: a ballot of the clamp test, then the wave prices each
+            // clamped option on its own range [min(a, xK - 0.1), max(b, xK + 0.1)] (lanes over
+            // k).  Mask words are written for every option, prices only for clamped ones; the
+            // option kernel trusts these bits, so the two kernels never disagree on a decision.
+            const int64_t slot0 = q * (int64_t)A.max_group;
+            for (int base = wv * 64; base < gn; base += kWaves * 64) {
+                const int o = base + lane;
+                bool cl = false;
+                double xK = 0.0, K = 0.0;
+                if (o < gn) {
+                    K = base == wv * 64 ? K_first : option_strike(A, g0 + o, S0);
+                    const double rq = K / S0;
+                    if (!(rq >= lo && rq <= hi)) {                   // near or past an edge
+                        double ratio;
+                        xK = option_logk(K, S0, ratio);
+                        cl = xK - 0.1 < a || xK + 0.1 > b;
+                    }
+                }
+                unsigned long long mask = __ballot(cl);
+                if (lane == 0) A.cl_mask[q * cl_words(A) + base / 64] = mask;
+                if (mask == 0) continue;
+                const int64_t p = A.p0 + q / tpp;
+                const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
+                const double disc = exp(-P.r * T);
+                while (mask) {
+                    const int l = __ffsll((long long)mask) - 1;
+                    mask &= mask - 1;
+                    const double x = __shfl(xK, l, 64);
+                    const double Kl = __shfl(K, l, 64);
+                    const int m = g0 + base + l;
+                    const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
+                    const double bc = (x + 0.1 > b) ? x + 0.1 : b;
+                    double v = clamped_term_sum(P, T, Kl, x, ac, bc, A.call[m] != 0, lane, 64, N);
+                    for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+                    if (lane == 0) A.cl_price[slot0 + base + l] = disc * v;
+                }
             }
         }
+        __syncthreads();
+        if (b0 == q_begin) DH_STAMP(A, 6);
+        // ---- fixed-order per-table sums of the batch ----
+        if (threadIdx.x < nb) {
+            const int i = threadIdx.x;
+            double sm[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int j = 0; j < 4; ++j)
+                for (int w = 0; w < kWaves; ++w) sm[j] += red[i][j][w];
+            const double* c = shc[i];
+            double* cs = A.consts + (b0 + i) * kConsts;
+            cs[0] = sm[0];
+            cs[1] = sm[1];
+            cs[2] = sm[2];
+            cs[3] = sm[3];
+            cs[4] = c[0];
+            cs[5] = c[1];
+            cs[6] = c[2];
+            cs[7] = c[3];
+        }
+        __syncthreads();
     }
     DH_STAMP(A, 7);
 }
@@ -748,6 +784,7 @@ struct dh_ctx {
     DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, cl_mask,
         cl_price, aux0, aux1, aux2, aux3;
     bool attr_set = false;
+    int table_resident[3] = {0, 0, 0};   // resident cos_table_kernel<64/128/256> blocks, chip
     int exact = 0;          // validation mode: every option through the per-term exact path
     int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
     DevBuf stamps;
@@ -789,6 +826,16 @@ int ensure_attrs(dh_ctx* ctx) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<256>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    // table-kernel grid = resident capacity (each block then owns a contiguous table range)
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const void* fns[3] = {(const void*)cos_table_kernel<64>, (const void*)cos_table_kernel<128>,
+                          (const void*)cos_table_kernel<256>};
+    for (int i = 0; i < 3; ++i) {
+        int per_cu = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fns[i], kBlock, 0));
+        ctx->table_resident[i] = std::max(1, per_cu) * std::max(1, cus);
+    }
     ctx->attr_set = true;
     return DH_OK;
 }
@@ -861,7 +908,8 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         A.cl_price = (double*)ctx->cl_price.ptr;
         A.stamps = ctx->stamps_on ? (unsigned long long*)ctx->stamps.ptr : nullptr;
         const int64_t n_q = A.np * tpp;
-        const int64_t b1 = (n_q + kBlock / t1 - 1) / (kBlock / t1);
+        const int res = ctx->table_resident[t1 == 64 ? 0 : (t1 == 128 ? 1 : 2)];
+        const int64_t b1 = std::min<int64_t>((n_q + kBlock / t1 - 1) / (kBlock / t1), res);
         const int64_t n_t = A.np * tasks_per_p;
         const int64_t b2 = (n_t + kBlock / t2 - 1) / (kBlock / t2);
         if (b1 > 0x7fffffffLL || b2 > 0x7fffffffLL) return fail(DH_E_ARG, "launch too large");
