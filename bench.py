@@ -180,10 +180,16 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream):
     G = 4
     flop = P * G * N * FLOP_TAB + P * M * (N - 1) * FLOP_TERM + P * M * FLOP_OPT
     alg_bytes = P * 16 * 8 + M * 17 + P * M * 8
+    # launch pairs per batch: the library chunks param sets so one chunk's tables stay within
+    # 256 MiB (dh_kernels.hip launch_price: per set = groups x (N + 8 consts + clamp words +
+    # largest group) doubles); the committed PMC bytes are per launch pair
+    per_p = G * (N + 8 + 1 + 8) * 8
+    n_chunks = -(-P // max(1, (256 << 20) // per_p))
+    tr = pmc_traffic(args.config)
     roofline = {"bound": "valu_fp64", "achieved": round(flop / (ker_ms * 1e-3) / 1e12, 3),
                 "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(flop / (ker_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4),
-                "traffic": pmc_traffic(args.config),
+                "traffic": tr * n_chunks if tr else None, "launch_pairs": n_chunks,
                 "kernel": "cos_table_kernel + cos_option_kernel (all chunks of one batch, HIP events)",
                 "kernel_ms": round(ker_ms, 4), "flop_per_launch": flop,
                 "alg_bytes_per_launch": alg_bytes,
