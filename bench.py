@@ -39,12 +39,19 @@ from dhcos.distributed import calibrate_sharded                # noqa: E402
 from dhcos.calibrator import (DoubleHestonJumpCalibrator,      # noqa: E402
                               fd_request_points, x_to_model)
 
-# Algorithmic work of the implemented algorithm in fp64 flop-equivalents (DESIGN.md "Roofline"),
-# frozen: add/mul = 1, fma = 2, and each elementary function = 2 x its gfx950 ocml instruction
-# count (exp 42, log 98, sin+cos 148, atan2 105, sqrt 22, div/rcp 12 instructions).
-FLOP_TAB = 3137        # per COS-table entry (p, T, k): fast-form CF + phase + T2..T4 + k-sums
-FLOP_TERM = 12         # per (param set, option, k >= 1): 3 fma + 1 complex rotation
-FLOP_OPT = 596         # per (param set, option): log, exp, step rotation, k = 0 term, loss
+# Algorithmic work = fp64 flops of the implemented algorithm (FMA = 2, add/mul = 1, each
+# elementary function at the flops its gfx950 implementation executes), frozen here
+# (DESIGN.md section 4):
+#   FLOP_TAB  per COS-table entry (p, T, k): fast-form CF, phase, T2/T4 k-sums -- the table
+#             kernel's executed fp64 flops per entry on C3 (rocprofv3 PMC, profiles/r01_c3_pmc.csv:
+#             1.807 GFLOP / 2,150,400 entries; 852 on C5)
+#   FLOP_TERM per (param set, option, k >= 1): 3 fma + one complex rotation (2 mul + 2 fma)
+#   FLOP_OPT  per (param set, option): log-strike, e^{i G th} sincos, final sum, loss term
+# The SURVEY 8(d) convention (716 per CF, 120 per option-term) is reported beside it; it charges
+# per-term trig the kernels replace by a rotation recurrence, so it exceeds the peak.
+FLOP_TAB = 840
+FLOP_TERM = 12
+FLOP_OPT = 110
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector peak (spec)
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BYTES_PER_OPTION = 8 + 8 + 1 + 8 + 4   # K, T, is_call, mkt, perm read per (param set, option)
@@ -153,7 +160,8 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream):
     torch.cuda.synchronize()
     chk = np.arange(0, P, P // 64)
     got = d_out[torch.from_numpy(chk).to(dev)].cpu().numpy()
-    assert np.array_equal(got, surf.price(host[chk], N)), "device/host path mismatch"
+    ref = surf.price(host[chk], N)          # a 64-set call: the large-tile kernel (last bits differ)
+    assert np.all(np.abs(got - ref) <= 1e-12 * np.abs(ref) + 1e-12), "device/host path mismatch"
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

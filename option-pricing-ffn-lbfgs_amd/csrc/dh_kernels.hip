@@ -617,6 +617,165 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
 }
 
 // ----------------------------------------------------------------------------------------------
+// option kernel, small tiles (<= kSmallTile options per tile): one lane carries kRs options of a
+// tile through every term k = 1 .. N-1.  Its step rotation e^{i th} is also its start angle, the
+// 8-byte table w_k is read straight from L2/MALL and expanded to (T2, T3, T4) on the fly
+// (amortised over kRs options), and a task's partial is reduced over its L lanes (L = lanes per
+// task, a power of two <= 4) before the same fence-free hand-off.  Per lane this is ~9 VALU
+// instructions per option-term with no LDS, no per-lane anchors and no butterflies -- the
+// large-tile kernel's fixed costs dominate when a tile has 5-16 options (generator grids).
+// ----------------------------------------------------------------------------------------------
+constexpr int kSmallTile = 16;
+constexpr int kRs = 4;
+// ...and only when a call has enough tasks to fill the chip with one lane group per task
+// (below this the large-tile kernel's many lanes per option win on latency).  Calibration
+// launches (14 x starts param sets) stay far below it, so lockstep == sequential bit for bit.
+constexpr int64_t kSmallMinTasks = 65536;
+
+__global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, int L) {
+    const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t n_tasks = A.paired ? A.np : A.np * (int64_t)A.n_tiles;
+    const int64_t task_l = gid / L;
+    const int sub = (int)(gid % L);
+    const bool active = task_l < n_tasks;
+    const int64_t p = A.p0 + (active ? (A.paired ? task_l : task_l / A.n_tiles) : 0);
+    const int tile = (active && !A.paired) ? (int)(task_l % A.n_tiles) : 0;
+    const int64_t task = A.paired ? p : p * A.n_tiles + tile;
+    int opt0 = 0, nopt = 0, g = 0;
+    if (active) {
+        if (A.paired) {
+            opt0 = (int)p;
+            nopt = 1;
+        } else {
+            const int2 tl = A.tiles[tile];
+            opt0 = tl.x;
+            nopt = tl.y;
+            g = A.tile_group[tile];
+        }
+    }
+    const int64_t q = (p - A.p0) * tabs_per_p(A) + g;
+    const double* prm = A.prm + p * DH_PARAM_STRIDE;
+    const double S0 = prm[13], r = prm[14];
+    Consts C{0.0, 0.0, 0.0, 0.0, 0.0, 1.0, 1.0, 1.0};
+    if (active) {
+        const double* cs = A.consts + q * kConsts;
+        C = Consts{cs[0], cs[1], cs[2], cs[3], cs[4], cs[5], cs[6], cs[7]};
+    }
+    const double ba = C.b - C.a;
+    const double piba = dh::kPi / ba;
+    const double T = active ? A.T[opt0] : 1.0;
+    const double disc = exp(-r * T);
+    const int g0 = A.paired ? (int)p : (active ? A.groups[g].x : 0);
+    const unsigned long long* msk = A.cl_mask + q * cl_words(A);
+    const double* clp = A.cl_price + q * (int64_t)A.max_group;
+
+    // per option: log-strike, clamp bit, start angle = step rotation e^{i th}
+    double dx[kRs], c[kRs], sn[kRs], cs[kRs], ss[kRs], s2[kRs], s4[kRs];
+    bool use[kRs];
+    double lsum = 0.0, lbad = 0.0;
+#pragma unroll
+    for (int j = 0; j < kRs; ++j) {
+        const int oi = sub * kRs + j;
+        const bool in = active && oi < nopt;
+        bool cl = false;
+        double xK = 0.0;
+        if (in) {
+            const int m = opt0 + oi;
+            const double K = option_strike(A, m, S0);
+            double ratio;
+            xK = option_logk(K, S0, ratio);
+            const int gpos = m - g0;
+            cl = (msk[gpos >> 6] >> (gpos & 63)) & 1ull;
+            if (cl) {                      // priced by the table kernel
+                const double price = clp[gpos];
+                if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
+                if (A.part_sse) {
+                    const double mk = A.mkt[m];
+                    const double rel = (price - mk) / mk;
+                    lsum += rel * rel;
+                    lbad += (isnan(price) || isinf(price) || price <= 0.0) ? 1.0 : 0.0;
+                }
+            }
+        }
+        use[j] = in && !cl;
+        dx[j] = use[j] ? xK - C.a : 0.0;
+        double s1, c1;
+        dh::dsincos(piba * dx[j], &s1, &c1);
+        cs[j] = c1;
+        ss[j] = s1;
+        c[j] = c1;
+        sn[j] = s1;
+        s2[j] = 0.0;
+        s4[j] = 0.0;
+    }
+    const double* tw = A.table + q * (int64_t)A.N;
+    int n = 0;
+    for (int k = 1; k < A.N; ++k, ++n) {
+        if (n == kAnchor) {
+            const double uk = k * piba;
+#pragma unroll
+            for (int j = 0; j < kRs; ++j) dh::dsincos(uk * dx[j], &sn[j], &c[j]);
+            n = 0;
+        }
+        const double w = active ? tw[k] : 0.0;
+        const double u = k * piba;
+        const double T2 = w * S0 * dh::drcp(1.0 + u * u);
+        const double T3 = T2 * u;
+        const double T4 = w * dh::drcp(u);
+#pragma unroll
+        for (int j = 0; j < kRs; ++j) {
+            s2[j] = fma(T2, c[j], s2[j]);
+            s2[j] = fma(T3, sn[j], s2[j]);
+            s4[j] = fma(T4, sn[j], s4[j]);
+            const double cn = c[j] * cs[j] - sn[j] * ss[j];
+            sn[j] = sn[j] * cs[j] + c[j] * ss[j];
+            c[j] = cn;
+        }
+    }
+    // finalise this lane's options, then the task partial over its L lanes (fixed tree)
+#pragma unroll
+    for (int j = 0; j < kRs; ++j) {
+        if (!use[j]) continue;
+        const int m = opt0 + sub * kRs + j;
+        const double K = option_strike(A, m, S0);
+        double ratio;
+        const double xK = option_logk(K, S0, ratio);
+        const double sum = option_sum(C, A.call[m] != 0, S0, K, xK, ratio, s2[j], s4[j]);
+        const double price = disc * sum;
+        if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
+        if (A.part_sse) {
+            const double mk = A.mkt[m];
+            const double rel = (price - mk) / mk;
+            lsum += rel * rel;
+            lbad += (isnan(price) || isinf(price) || price <= 0.0) ? 1.0 : 0.0;
+        }
+    }
+    if (!A.part_sse) return;
+    for (int off = 1; off < L; off <<= 1) {
+        lsum += __shfl_xor(lsum, off, 64);
+        lbad += __shfl_xor(lbad, off, 64);
+    }
+    if (!active || sub != 0) return;
+    // fence-free hand-off (as task_loss): sc1 stores, drain, agent-scope ticket
+    __hip_atomic_store(&A.part_sse[task], lsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&A.part_bad[task], (int)lbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old =
+        __hip_atomic_fetch_add(&A.counter[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old != (unsigned)A.n_tiles - 1u) return;
+    const int64_t base_i = p * A.n_tiles;
+    double acc = 0.0;
+    int bad = 0;
+    for (int j = 0; j < A.n_tiles; ++j) {           // tile order
+        acc += __hip_atomic_load(&A.part_sse[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bad += __hip_atomic_load(&A.part_bad[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    A.sse[p] = acc;
+    A.n_bad[p] = bad;
+    __hip_atomic_store(&A.counter[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ----------------------------------------------------------------------------------------------
 // validation path: reference operation order (double_heston.py:160-192), one wave per option
 // ----------------------------------------------------------------------------------------------
 __device__ __forceinline__ double exact_term_sum(const Params& P, double T, double K, double xK,
@@ -888,8 +1047,14 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     HIP_TRY(ctx->cl_price.reserve((size_t)chunk * tpp * A0.max_group * sizeof(double)));
     const int t1 = table_tpt(N);
     const int max_nopt = A0.paired ? 1 : A0.opt_cap;
-    const int t2 = option_tpt(max_nopt, N, A0.opt_cap);
-    const size_t lds2 = (size_t)(kBlock / t2) * option_lds_doubles(N, A0.opt_cap) * sizeof(double);
+    // small tiles in a large call take the lane-per-option-group kernel (decided once per call,
+    // so every chunk of it runs the same arithmetic)
+    const bool small = max_nopt <= kSmallTile && A0.P * tasks_per_p >= kSmallMinTasks;
+    int L = 1;
+    while (L * kRs < max_nopt) L *= 2;
+    const int t2 = small ? kBlock : option_tpt(max_nopt, N, A0.opt_cap);
+    const size_t lds2 =
+        small ? 0 : (size_t)(kBlock / t2) * option_lds_doubles(N, A0.opt_cap) * sizeof(double);
     if (lds2 > (size_t)kLdsMax) return fail(DH_E_ARG, "COS table does not fit in LDS");
     if (ctx->stamps_on) {
         const int64_t nb = std::max((chunk * tasks_per_p + kBlock / t2 - 1) / (kBlock / t2),
@@ -911,7 +1076,8 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         const int res = ctx->table_resident[t1 == 64 ? 0 : (t1 == 128 ? 1 : 2)];
         const int64_t b1 = std::min<int64_t>((n_q + kBlock / t1 - 1) / (kBlock / t1), res);
         const int64_t n_t = A.np * tasks_per_p;
-        const int64_t b2 = (n_t + kBlock / t2 - 1) / (kBlock / t2);
+        const int64_t b2 = small ? (n_t * L + kBlock - 1) / kBlock
+                                 : (n_t + kBlock / t2 - 1) / (kBlock / t2);
         if (b1 > 0x7fffffffLL || b2 > 0x7fffffffLL) return fail(DH_E_ARG, "launch too large");
         switch (t1) {
             case 64: hipLaunchKernelGGL(cos_table_kernel<64>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
@@ -919,7 +1085,9 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
             default: hipLaunchKernelGGL(cos_table_kernel<256>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
         }
         HIP_TRY(hipGetLastError());
-        switch (t2) {
+        if (small) {
+            hipLaunchKernelGGL(cos_option_small_kernel, dim3((unsigned)b2), dim3(kBlock), 0, st, A, L);
+        } else switch (t2) {
             case 64: hipLaunchKernelGGL(cos_option_kernel<64>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;
             case 128: hipLaunchKernelGGL(cos_option_kernel<128>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;
             default: hipLaunchKernelGGL(cos_option_kernel<256>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;

@@ -397,3 +397,39 @@ def test_clamped_options_across_mask_words_and_tiles(dh):
     assert rel_close(got, exact, 1e-11, 1e-11).all(), np.max(np.abs(got - exact))
     pairs = ctx.price_pairs(np.repeat(rec[:1], len(far), 0), K[far], T[far], call[far], N)
     assert rel_close(pairs, want[0, far], FID_RTOL, BAR_ATOL).all()
+
+
+def test_small_tile_path_large_call(dh):
+    """Calls with >= 65,536 tasks on surfaces whose tiles hold <= 16 options (generator grids)
+    run the lane-per-option-group kernel.  Its prices must agree with the large-tile kernel
+    (the same rows priced in a small call) and with the oracle, including clamp-widened
+    strikes, and its loss must be the loss of its own prices."""
+    from dhcos import _native
+    rs = np.random.RandomState(33)
+    P, N = 16500, 128                                   # 16,500 x 4 maturity tiles = 66,000 tasks
+    Krel = np.concatenate([np.tile(np.linspace(80.0, 120.0, 8), 4), [3.0, 900.0]])
+    T = np.concatenate([np.repeat([0.25, 0.5, 1.0, 2.0], 8), [0.25, 0.25]])
+    call = np.ones(T.size, dtype=np.int8)
+    call[::3] = 0
+    lo = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
+    hi = np.array([0.08, 4.5, 0.065, 0.5, -0.4, 0.07, 1.2, 0.07, 0.35, -0.2, 0.25, -0.01, 0.12])
+    rec = np.zeros((P, 16))
+    rec[:, :13] = lo + (hi - lo) * rs.rand(P, 13)
+    rec[:, 13] = 100.0 * np.exp(rs.normal(0, 0.05, P))
+    rec[:, 14] = 0.03
+    ctx = _native.default_context()
+    mkt = 1.0 + rs.rand(T.size)
+    surf = _native.Surface(ctx, Krel, T, call, mkt, strike_mode=_native.STRIKE_PCT_SPOT)
+    big = surf.price(rec, N)
+    rows = np.sort(rs.choice(P, 48, replace=False))
+    ref_path = surf.price(rec[rows], N)                 # 48 x 5 tasks: large-tile kernel
+    assert rel_close(big[rows], ref_path, 1e-12, 1e-12).all(), np.max(np.abs(big[rows] - ref_path))
+    for rr in rows[:6]:
+        want = O.price_many(rec[rr, :13], rec[rr, 13], Krel * rec[rr, 13] / 100.0, T, 0.03,
+                            call.astype(bool), N)
+        assert rel_close(big[rr], want, FID_RTOL, BAR_ATOL).all(), (rr, big[rr] - want)
+    sse, bad, prices = surf.loss_terms(rec, N, want_prices=True)
+    assert np.array_equal(prices, big)
+    ref_sse = np.sum(((big - mkt) / mkt) ** 2, axis=1)
+    assert rel_close(sse, ref_sse, 1e-12, 0).all()
+    assert np.array_equal(bad, np.sum(~(big > 0) | ~np.isfinite(big), axis=1))
