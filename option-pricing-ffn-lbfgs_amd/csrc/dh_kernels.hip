@@ -236,7 +236,6 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             // strike of this lane's first clamp-scan option, loaded now, used after the CF loop
             const int o_first = wv * 64 + lane;
             const double K_first = o_first < gn ? option_strike(A, g0 + o_first, S0) : 0.0;
-            const double ba = b - a;
             double* tw = A.table + q * (int64_t)N;
             double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
             for (int k = t; k < N; k += TPT) {
@@ -247,12 +246,12 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                     w0 = 0.5 * w;
                     continue;
                 }
-                double sb, cb;
-                dh::dsincos(u * ba, &sb, &cb);
+                // chi_k / psi_k at d = b: u (b - a) = k pi, so cos = (-1)^k and sin = 0 exactly
+                // (the reference evaluates them with ~1e-16 rounding noise; c1 = sum T4 sin(.)
+                // is therefore 0 and kept only for the consts layout)
+                const double cb = (k & 1) ? -1.0 : 1.0;
                 const double T2 = w * S0 * dh::drcp(1.0 + u * u);
-                const double T4 = w * dh::drcp(u);
-                c0 += T2 * eb * (cb + u * sb);
-                c1 += T4 * sb;
+                c0 += T2 * eb * cb;
                 c5 += T2 * ea;
             }
             for (int off = 1; off < 64; off <<= 1) {
