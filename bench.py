@@ -107,6 +107,13 @@ def cpu_baseline(cal_opts, S0, r, N, budget_s=12.0):
                       f"oracle.dh_oracle.price_scalar (reference algorithm restated) in {dt:.1f} s"}
 
 
+def kernel_label(ctx):
+    """Kernels of the last request on ctx (after the bench's own launches)."""
+    if ctx.last_path == _native.PATH_FUSED:
+        return "cos_fused_kernel"
+    return "cos_table_kernel + cos_option[_small]_kernel"
+
+
 def pmc_traffic(config):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -198,7 +205,7 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream):
                 "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(flop / (ker_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4),
                 "traffic": tr * n_chunks if tr else None, "launch_pairs": n_chunks,
-                "kernel": "cos_table_kernel + cos_option_kernel (all chunks of one batch, HIP events)",
+                "kernel": kernel_label(surf.ctx) + " (all chunks of one batch, HIP events)",
                 "kernel_ms": round(ker_ms, 4), "flop_per_launch": flop,
                 "alg_bytes_per_launch": alg_bytes,
                 "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
@@ -233,6 +240,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-calib", action="store_true", help="skip the full-calibration leg")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--path", default="auto", choices=["auto", "split", "fused"],
+                    help="request kernels (libdhcos dh_ctx_set_path): auto, table+option "
+                         "launches, or one fused launch")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N > 1 "
                          "with several ranks on one GPU)")
@@ -252,6 +262,8 @@ def main():
     dev = torch.device("cuda", local)
     coll = dev if args.backend == "nccl" else torch.device("cpu")   # collective tensors
     os.environ["DHCOS_DEVICE"] = str(local)
+    _native.default_context().set_path({"auto": _native.PATH_AUTO, "split": _native.PATH_SPLIT,
+                                        "fused": _native.PATH_FUSED}[args.path])
     # a dedicated (non-null) stream: libdhcos launches on it and the HIP events time it
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
@@ -332,7 +344,7 @@ def main():
     roofline = {"bound": "valu_fp64", "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4),
                 "traffic": pmc_traffic(args.config),
-                "kernel": "cos_table_kernel + cos_option_kernel (one request, HIP events)",
+                "kernel": kernel_label(surf.ctx) + " (one request, HIP events)",
                 "kernel_ms": round(ker_ms, 5), "flop_per_launch": flop,
                 "alg_bytes_per_launch": alg_bytes,
                 "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),

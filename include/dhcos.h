@@ -65,6 +65,15 @@ void* dh_ctx_stream(dh_ctx* ctx);
 /* Validation mode: when on, every option is priced by the per-term path in the reference's
  * operation order (own CF and sincos per COS term) instead of the shared-table fast path.   */
 int dh_ctx_set_exact(dh_ctx* ctx, int on);
+/* Request kernels of the fast path.  AUTO (default): one fused launch per request when every
+ * maturity group fits one tile (<= 256 options) and the request has at most 1,024 (param set,
+ * maturity) tables (latency-bound calibration requests), else a COS-table launch then an option
+ * launch.  FUSED / SPLIT force one of the two where it
+ * applies.  Both produce the same bits; the choice only changes speed.                      */
+enum { DH_PATH_AUTO = 0, DH_PATH_SPLIT = 1, DH_PATH_FUSED = 2 };
+int dh_ctx_set_path(dh_ctx* ctx, int path);
+/* DH_PATH_FUSED or DH_PATH_SPLIT: the kernels the last fast-path request ran (0 before any). */
+int dh_ctx_last_path(dh_ctx* ctx);
 /* Diagnostics (only in the DH_STAMPS build, `make stamps`; the production library returns
  * DH_E_ARG): record per-block s_memtime phase stamps of the COS kernels, read the last request's. */
 int dh_ctx_debug_stamps(dh_ctx* ctx, int on);
@@ -99,8 +108,8 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
 
 /* Device-pointer variants: params/out/sse/n_bad are device pointers; enqueue on `stream`
  * (hipStream_t; NULL = context stream).  No synchronisation, no allocation after warm-up.
- * A request is two kernel launches (COS table, then options + fused loss: the last task of each
- * param set finalises its sum in a fixed order).
+ * A request is one fused launch or two launches (COS table, then options), dh_ctx_set_path;
+ * in loss mode the last task of each param set finalises its sum in a fixed order.
  * Launches through one context share its scratch: issue them on one stream at a time.       */
 int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int64_t P,
                          int N, double L, double* d_out, void* stream);

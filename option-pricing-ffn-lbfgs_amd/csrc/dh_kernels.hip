@@ -155,6 +155,38 @@ constexpr int kTabC = 29;
 constexpr double kClampMargin = 1e-9;   // relative safety margin of the K-space prefilter
 static_assert(sizeof(dh::CfConsts) == 16 * sizeof(double), "CfConsts layout");
 
+// Prologue of table q = (p, g) of a launch: truncation range, CF constants and the staged values
+// above, written to c[0 .. kTabC).
+__device__ __forceinline__ void table_prologue(const PriceArgs& A, int64_t q, double* c) {
+    const int tpp = tabs_per_p(A);
+    const int64_t p = A.p0 + q / tpp;
+    const int g = (int)(q % tpp);
+    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
+    const double T = A.paired ? A.T[p] : A.group_T[g];
+    int2 gr = make_int2((int)p, 1);
+    if (!A.paired) gr = A.groups[g];
+    double a, b;
+    dh::trunc_unclamped(P, T, A.L, a, b);            // double_heston.py:100-132
+    const dh::CfConsts CC = dh::cf_consts(P, T);
+    c[0] = a;
+    c[1] = b;
+    c[2] = exp(b);
+    c[3] = exp(a);
+    c[4] = 2.0 / (b - a);
+    c[5] = dh::kPi / (b - a);
+    const double* cc = (const double*)&CC;
+    for (int i = 0; i < 16; ++i) c[6 + i] = cc[i];
+    c[22] = P.S0;
+    c[23] = P.r;
+    c[24] = T;
+    // unclamped iff a + 0.1 <= log(K/S0) <= b - 0.1: strikes whose K/S0 is inside these
+    // bounds by a 1e-9 relative margin cannot be clamped (exp/log errors are ~1e-16)
+    c[25] = exp(a + 0.1) * (1.0 + kClampMargin);
+    c[26] = exp(b - 0.1) * (1.0 - kClampMargin);
+    c[27] = gr.x;
+    c[28] = gr.y;
+}
+
 #ifndef DH_TABLE_WAVES
 #define DH_TABLE_WAVES 2    // min waves per SIMD: caps VGPR+AGPR at 256 (the CF needs ~250)
 #endif
@@ -189,36 +221,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
     for (int64_t b0 = q_begin; b0 < q_end; b0 += kBatch) {
         const int nb = (int)min<int64_t>(kBatch, q_end - b0);
         // ---- prologue, one lane per table: truncation range and CF constants ----
-        if (threadIdx.x < nb) {
-            const int64_t q = b0 + threadIdx.x;
-            const int64_t p = A.p0 + q / tpp;
-            const int g = (int)(q % tpp);
-            const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
-            const double T = A.paired ? A.T[p] : A.group_T[g];
-            int2 gr = make_int2((int)p, 1);
-            if (!A.paired) gr = A.groups[g];
-            double a, b;
-            dh::trunc_unclamped(P, T, A.L, a, b);            // double_heston.py:100-132
-            const dh::CfConsts CC = dh::cf_consts(P, T);
-            double* c = shc[threadIdx.x];
-            c[0] = a;
-            c[1] = b;
-            c[2] = exp(b);
-            c[3] = exp(a);
-            c[4] = 2.0 / (b - a);
-            c[5] = dh::kPi / (b - a);
-            const double* cc = (const double*)&CC;
-            for (int i = 0; i < 16; ++i) c[6 + i] = cc[i];
-            c[22] = P.S0;
-            c[23] = P.r;
-            c[24] = T;
-            // unclamped iff a + 0.1 <= log(K/S0) <= b - 0.1: strikes whose K/S0 is inside these
-            // bounds by a 1e-9 relative margin cannot be clamped (exp/log errors are ~1e-16)
-            c[25] = exp(a + 0.1) * (1.0 + kClampMargin);
-            c[26] = exp(b - 0.1) * (1.0 - kClampMargin);
-            c[27] = gr.x;
-            c[28] = gr.y;
-        }
+        if (threadIdx.x < nb) table_prologue(A, b0 + threadIdx.x, shc[threadIdx.x]);
         __syncthreads();
         if (b0 == q_begin) DH_STAMP(A, 5);
 
@@ -448,6 +451,114 @@ __host__ __device__ constexpr int option_lds_doubles(int N, int opt_cap) {
     return 4 * N + 8 * opt_cap + ((2 * opt_cap + 3) / 4) * 2;
 }
 
+// LDS view of one staged tile: the expanded (p, g) table and the per-option arrays
+struct TileLds {
+    double2* t23;
+    double* t4;
+    double* tu;
+    double* K;
+    double* mkt;
+    double* sse;
+    double* bad;
+    double* xK;       // log(K / S0)
+    double* exK;      // e^{log(K / S0)}
+    double* cs;       // cos / sin of the G-step rotation (sin = NaN marks a clamped option)
+    double* ss;
+    int* call;
+    int* perm;
+};
+
+__device__ __forceinline__ TileLds tile_lds(double* base, int N, int cap) {
+    TileLds L;
+    L.t23 = (double2*)base;
+    L.t4 = base + 2 * N;
+    L.tu = base + 3 * N;
+    L.K = base + 4 * N;
+    L.mkt = L.K + cap;
+    L.sse = L.mkt + cap;
+    L.bad = L.sse + cap;
+    L.xK = L.bad + cap;
+    L.exK = L.xK + cap;
+    L.cs = L.exK + cap;
+    L.ss = L.cs + cap;
+    L.call = (int*)(L.ss + cap);
+    L.perm = L.call + cap;
+    return L;
+}
+
+// lanes per group of kR options for a tile of nopt options priced by tpt threads
+__device__ __forceinline__ int group_lanes(int nopt, int N, int tpt) {
+    const int R = min(kR, max(nopt, 1));
+    const int ngroups = (nopt + R - 1) / R;
+    int G = 1;
+    while (G * 2 <= tpt / max(ngroups, 1) && G < 64) G *= 2;
+    while (G > 1 && G / 2 >= N - 1) G /= 2;                 // no more lanes than terms k >= 1
+    return G;
+}
+
+// Angle sums, finalisation and price / loss-term recording of one staged tile (thread t of the
+// tile's tpt).  Shared by cos_option_kernel and cos_fused_kernel, so both give the same bits.
+__device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const Consts& C,
+                                          double S0, double disc, int nopt, int G, int tpt, int t,
+                                          bool active, const TileLds& L) {
+    const int N = A.N;
+    const int R = min(kR, max(nopt, 1));
+    const int ngroups = (nopt + R - 1) / R;
+    const int groups_per_pass = tpt / G;
+    for (int pass = 0; pass < ngroups; pass += groups_per_pass) {
+        const int gi = pass + t / G;
+        const int gl = t % G;
+        const bool gvalid = active && gi < ngroups;
+        double dx[kR], cs[kR], ss[kR];
+        bool use[kR];
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+            const int oi = gi * R + j;
+            const bool in = gvalid && j < R && oi < nopt;
+            const double sj = in ? L.ss[oi] : 0.0;
+            use[j] = in && !isnan(sj);                               // clamped: recorded
+            dx[j] = use[j] ? L.xK[oi] - C.a : 0.0;
+            cs[j] = use[j] ? L.cs[oi] : 1.0;
+            ss[j] = use[j] ? sj : 0.0;
+        }
+        double s2[kR], s4[kR];
+        angle_sums_r(1 + gl, G, N, dx, cs, ss, L.tu, L.t23, L.t4, s2, s4);
+        for (int off = 1; off < G; off <<= 1) {
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {
+                s2[j] += __shfl_xor(s2[j], off, 64);
+                s4[j] += __shfl_xor(s4[j], off, 64);
+            }
+        }
+        // every lane of the group holds the (bitwise identical) sums: lane j finalises option j
+        if (G >= R) {
+            double m2 = s2[0], m4 = s4[0];
+            bool mu = use[0];
+#pragma unroll
+            for (int j = 1; j < kR; ++j) {
+                m2 = gl == j ? s2[j] : m2;
+                m4 = gl == j ? s4[j] : m4;
+                mu = gl == j ? use[j] : mu;
+            }
+            if (gl < R && mu) {
+                const int oi = gi * R + gl;
+                const double sum = option_sum(C, L.call[oi] != 0, S0, L.K[oi], L.xK[oi],
+                                              L.exK[oi], m2, m4);
+                record_price(A, p, L.perm[oi], L.mkt[oi], oi, disc * sum, L.sse, L.bad);
+            }
+        } else if (gl == 0) {
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {
+                if (!use[j]) continue;
+                const int oi = gi * R + j;
+                const double sum = option_sum(C, L.call[oi] != 0, S0, L.K[oi], L.xK[oi],
+                                              L.exK[oi], s2[j], s4[j]);
+                record_price(A, p, L.perm[oi], L.mkt[oi], oi, disc * sum, L.sse, L.bad);
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------------------
 // option kernel
 // ----------------------------------------------------------------------------------------------
@@ -468,20 +579,20 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     DH_STAMP(A, 0);
 
     const int cap = A.opt_cap;
-    double* base = smem + (size_t)slot * option_lds_doubles(N, cap);
-    double2* t23 = (double2*)base;
-    double* t4 = base + 2 * N;
-    double* tu = base + 3 * N;
-    double* lK = base + 4 * N;
-    double* lmkt = lK + cap;
-    double* lsse = lmkt + cap;
-    double* lbad = lsse + cap;
-    double* lxK = lbad + cap;                          // log(K / S0)
-    double* lexK = lxK + cap;                          // e^{log(K / S0)}
-    double* lcs = lexK + cap;                          // cos / sin of the G-step rotation
-    double* lss = lcs + cap;
-    int* lcall = (int*)(lss + cap);
-    int* lperm = lcall + cap;
+    const TileLds L = tile_lds(smem + (size_t)slot * option_lds_doubles(N, cap), N, cap);
+    double2* t23 = L.t23;
+    double* t4 = L.t4;
+    double* tu = L.tu;
+    double* lK = L.K;
+    double* lmkt = L.mkt;
+    double* lsse = L.sse;
+    double* lbad = L.bad;
+    double* lxK = L.xK;
+    double* lexK = L.exK;
+    double* lcs = L.cs;
+    double* lss = L.ss;
+    int* lcall = L.call;
+    int* lperm = L.perm;
 
     int opt0 = 0, nopt = 0, g = 0;
     if (active) {
@@ -496,11 +607,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
         }
     }
     // lanes: groups of kR options on G lanes each
-    const int R = min(kR, max(nopt, 1));
-    const int ngroups = (nopt + R - 1) / R;
-    int G = 1;
-    while (G * 2 <= TPT / max(ngroups, 1) && G < 64) G *= 2;
-    while (G > 1 && G / 2 >= N - 1) G /= 2;                 // no more lanes than terms k >= 1
+    const int G = group_lanes(nopt, N, TPT);
 
     const int64_t q = (p - A.p0) * tabs_per_p(A) + g;
     const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
@@ -552,59 +659,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     __syncthreads();
     DH_STAMP(A, 1);
 
-    const int groups_per_pass = TPT / G;
-    for (int pass = 0; pass < ngroups; pass += groups_per_pass) {
-        const int gi = pass + t / G;
-        const int gl = t % G;
-        const bool gvalid = active && gi < ngroups;
-        double dx[kR], cs[kR], ss[kR];
-        bool use[kR];
-#pragma unroll
-        for (int j = 0; j < kR; ++j) {
-            const int oi = gi * R + j;
-            const bool in = gvalid && j < R && oi < nopt;
-            const double sj = in ? lss[oi] : 0.0;
-            use[j] = in && !isnan(sj);                               // clamped: recorded
-            dx[j] = use[j] ? lxK[oi] - C.a : 0.0;
-            cs[j] = use[j] ? lcs[oi] : 1.0;
-            ss[j] = use[j] ? sj : 0.0;
-        }
-        double s2[kR], s4[kR];
-        angle_sums_r(1 + gl, G, N, dx, cs, ss, tu, t23, t4, s2, s4);
-        for (int off = 1; off < G; off <<= 1) {
-#pragma unroll
-            for (int j = 0; j < kR; ++j) {
-                s2[j] += __shfl_xor(s2[j], off, 64);
-                s4[j] += __shfl_xor(s4[j], off, 64);
-            }
-        }
-        // every lane of the group holds the (bitwise identical) sums: lane j finalises option j
-        if (G >= R) {
-            double m2 = s2[0], m4 = s4[0];
-            bool mu = use[0];
-#pragma unroll
-            for (int j = 1; j < kR; ++j) {
-                m2 = gl == j ? s2[j] : m2;
-                m4 = gl == j ? s4[j] : m4;
-                mu = gl == j ? use[j] : mu;
-            }
-            if (gl < R && mu) {
-                const int oi = gi * R + gl;
-                const double sum = option_sum(C, lcall[oi] != 0, P.S0, lK[oi], lxK[oi], lexK[oi],
-                                              m2, m4);
-                record_price(A, p, lperm[oi], lmkt[oi], oi, disc * sum, lsse, lbad);
-            }
-        } else if (gl == 0) {
-#pragma unroll
-            for (int j = 0; j < kR; ++j) {
-                if (!use[j]) continue;
-                const int oi = gi * R + j;
-                const double sum = option_sum(C, lcall[oi] != 0, P.S0, lK[oi], lxK[oi], lexK[oi],
-                                              s2[j], s4[j]);
-                record_price(A, p, lperm[oi], lmkt[oi], oi, disc * sum, lsse, lbad);
-            }
-        }
-    }
+    tile_sums(A, p, C, P.S0, disc, nopt, G, TPT, t, active, L);
     DH_STAMP(A, 2);
 
     // ---- loss: fixed-order per-task partial, last arriver finalises the param set ----
@@ -772,6 +827,165 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
     A.sse[p] = acc;
     A.n_bad[p] = bad;
     __hip_atomic_store(&A.counter[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ----------------------------------------------------------------------------------------------
+// fused request kernel: one block per table (p, g) whose maturity group is one tile.
+//   prologue (thread 0) || option staging (other waves first) -> CF loop writing the expanded
+//   table straight into LDS + k-sums -> clamp scan -> fixed-order constants || rotations ->
+//   tile sums -> fence-free loss hand-off.
+// One launch and no table round trip through L2/MALL: the latency path of small requests
+// (calibration function+gradient requests).  Every value is computed by the same expression, in
+// the same order and with the same lane partition as cos_table_kernel<TPT1> followed by
+// cos_option_kernel<tpt2>, so the two paths give the same bits.
+// ----------------------------------------------------------------------------------------------
+template <int TPT1>
+__global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(PriceArgs A, int tpt2) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    __shared__ double shc[kTabC];
+    __shared__ double red[4][kBlock / 64];
+    __shared__ unsigned long long cmask[kTileMax / 64];
+    const int nthr = blockDim.x;
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wv = t >> 6;
+    const int N = A.N;
+    const int tpp = tabs_per_p(A);
+    const int64_t q = blockIdx.x;
+    const int64_t p = A.p0 + q / tpp;
+    const int g = (int)(q % tpp);
+    const int cap = A.opt_cap;
+    const TileLds L = tile_lds(smem, N, cap);
+    double* lclp = smem + option_lds_doubles(N, cap);     // prices of clamp-widened options
+    int g0, gn;
+    if (A.paired) {
+        g0 = (int)p;
+        gn = 1;
+    } else {
+        const int2 gr = A.groups[g];
+        g0 = gr.x;
+        gn = gr.y;
+    }
+    const double* prm = A.prm + p * DH_PARAM_STRIDE;
+    const double S0 = prm[13];
+    DH_STAMP(A, 0);
+
+    // ---- prologue (thread 0) || per-option staging (wave 0 takes the last indices) ----
+    if (t == 0) table_prologue(A, q, shc);
+    for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
+        const int m = g0 + i;
+        const double K = option_strike(A, m, S0);
+        double ratio;
+        const double xK = option_logk(K, S0, ratio);
+        L.K[i] = K;
+        L.mkt[i] = A.mkt ? A.mkt[m] : 0.0;
+        L.call[i] = A.call[m];
+        L.perm[i] = A.perm[m];
+        L.xK[i] = xK;
+        L.exK[i] = ratio;
+    }
+    __syncthreads();
+    DH_STAMP(A, 1);
+
+    const double a = shc[0], b = shc[1], eb = shc[2], ea = shc[3], scale = shc[4], piba = shc[5];
+    const double T = shc[24];
+    // ---- CF loop (threads < TPT1, as cos_table_kernel<TPT1>): expanded table into LDS ----
+    if (t < TPT1) {
+        dh::CfConsts CC;
+        {
+            double* cc = (double*)&CC;
+            for (int j = 0; j < 16; ++j) cc[j] = shc[6 + j];
+        }
+        double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
+        for (int k = t; k < N; k += TPT1) {
+            const double u = k * piba;
+            const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+            L.tu[k] = u;
+            if (k == 0) {
+                w0 = 0.5 * w;
+                L.t23[0] = make_double2(0.0, 0.0);
+                L.t4[0] = 0.0;
+                continue;
+            }
+            const double cb = (k & 1) ? -1.0 : 1.0;
+            const double T2 = w * S0 * dh::drcp(1.0 + u * u);
+            c0 += T2 * eb * cb;
+            c5 += T2 * ea;
+            L.t23[k] = make_double2(T2, T2 * u);
+            L.t4[k] = w * dh::drcp(u);
+        }
+        for (int off = 1; off < 64; off <<= 1) {
+            c0 += __shfl_xor(c0, off, 64);
+            c1 += __shfl_xor(c1, off, 64);
+            c5 += __shfl_xor(c5, off, 64);
+            w0 += __shfl_xor(w0, off, 64);
+        }
+        if (lane == 0) {
+            red[0][wv] = c0;
+            red[1][wv] = c1;
+            red[2][wv] = c5;
+            red[3][wv] = w0;
+        }
+    }
+    // ---- clamp-widened options (double_heston.py:135-137), decided and priced per wave ----
+    for (int base = wv * 64; base < gn; base += nthr) {
+        const int o = base + lane;
+        bool cl = false;
+        if (o < gn) {
+            const double xK = L.xK[o];
+            cl = xK - 0.1 < a || xK + 0.1 > b;
+        }
+        unsigned long long mask = __ballot(cl);
+        if (lane == 0) cmask[base / 64] = mask;
+        if (mask == 0) continue;
+        const Params P = dh::load_params(prm);
+        const double disc = exp(-P.r * T);
+        while (mask) {
+            const int l = __ffsll((long long)mask) - 1;
+            mask &= mask - 1;
+            const double x = L.xK[base + l];
+            const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
+            const double bc = (x + 0.1 > b) ? x + 0.1 : b;
+            double v = clamped_term_sum(P, T, L.K[base + l], x, ac, bc, L.call[base + l] != 0,
+                                        lane, 64, N);
+            for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+            if (lane == 0) lclp[base + l] = disc * v;
+        }
+    }
+    __syncthreads();
+    DH_STAMP(A, 2);
+
+    // ---- fixed-order constants (as the table kernel) || per-option rotations ----
+    Consts C;
+    {
+        double sm[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < 4; ++j)
+            for (int w = 0; w < TPT1 / 64; ++w) sm[j] += red[j][w];
+        C = Consts{sm[0], sm[1], sm[2], sm[3], a, b, eb, ea};
+    }
+    const double disc = exp(-prm[14] * T);
+    const int G = group_lanes(gn, N, tpt2);
+    {
+        const double ustep = G * dh::kPi / (C.b - C.a);
+        for (int i = t; i < gn; i += nthr) {
+            const bool cl = (cmask[i >> 6] >> (i & 63)) & 1ull;
+            double ss, cs;
+            dh::dsincos(ustep * (cl ? 0.0 : L.xK[i] - C.a), &ss, &cs);
+            L.cs[i] = cs;
+            L.ss[i] = cl ? NAN : ss;
+            if (cl) record_price(A, p, L.perm[i], L.mkt[i], i, lclp[i], L.sse, L.bad);
+        }
+    }
+    __syncthreads();
+    DH_STAMP(A, 3);
+
+    if (t < tpt2) tile_sums(A, p, C, S0, disc, gn, G, tpt2, t, true, L);
+    DH_STAMP(A, 4);
+    if (A.part_sse) {
+        __syncthreads();
+        if (t < 64) task_loss(A, p, A.paired ? p : p * A.n_tiles + g, gn, t, L.sse, L.bad);
+    }
+    DH_STAMP(A, 5);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -944,6 +1158,8 @@ struct dh_ctx {
     bool attr_set = false;
     int table_resident[3] = {0, 0, 0};   // resident cos_table_kernel<64/128/256> blocks, chip
     int exact = 0;          // validation mode: every option through the per-term exact path
+    int path = DH_PATH_AUTO;   // fused / split request kernels (dh_ctx_set_path)
+    int last_path = 0;         // kernels of the last fast-path request (dh_ctx_last_path)
     int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
     DevBuf stamps;
     int64_t stamps_n = 0;
@@ -984,6 +1200,9 @@ int ensure_attrs(dh_ctx* ctx) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<256>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    for (const void* f : {(const void*)cos_fused_kernel<64>, (const void*)cos_fused_kernel<128>,
+                          (const void*)cos_fused_kernel<256>})
+        HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax - 4096));
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -1026,8 +1245,44 @@ int launch_exact(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
     return DH_OK;
 }
 
+constexpr int64_t kFusedMaxTables = 1024;   // auto path: fused up to this many (p, g) tables
+
+size_t fused_lds_bytes(int N, int cap) {
+    return ((size_t)option_lds_doubles(N, cap) + (size_t)cap) * sizeof(double);
+}
+
+// One fused launch for the whole request (every group is one tile).
+int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
+    const int N = A0.N;
+    const int tpp = A0.paired ? 1 : A0.n_groups;
+    const int t1 = table_tpt(N);
+    const int max_nopt = A0.paired ? 1 : A0.opt_cap;
+    const int t2 = option_tpt(max_nopt, N, A0.opt_cap);
+    const size_t lds = fused_lds_bytes(N, A0.opt_cap);
+    const int64_t blocks = A0.P * tpp;
+    if (blocks > 0x7fffffffLL) return fail(DH_E_ARG, "launch too large");
+    PriceArgs A = A0;
+    A.p0 = 0;
+    A.np = A0.P;
+    if (ctx->stamps_on) {
+        HIP_TRY(ctx->stamps.reserve((size_t)blocks * kStamps * 8));
+        HIP_TRY(hipMemsetAsync(ctx->stamps.ptr, 0, (size_t)blocks * kStamps * 8, st));
+        ctx->stamps_n = blocks * kStamps;
+        A.stamps = (unsigned long long*)ctx->stamps.ptr;
+    }
+    const dim3 grid((unsigned)blocks), block((unsigned)std::max(t1, t2));
+    switch (t1) {
+        case 64: hipLaunchKernelGGL(cos_fused_kernel<64>, grid, block, lds, st, A, t2); break;
+        case 128: hipLaunchKernelGGL(cos_fused_kernel<128>, grid, block, lds, st, A, t2); break;
+        default: hipLaunchKernelGGL(cos_fused_kernel<256>, grid, block, lds, st, A, t2); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return DH_OK;
+}
+
 // Table kernel then option kernel per chunk of param sets; the chunk keeps the table workspace
-// within kTableBudget (L2/MALL-resident between the two launches).
+// within kTableBudget (L2/MALL-resident between the two launches).  Requests whose maturity
+// groups are single tiles may instead run as one fused launch (ctx->path).
 int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     const int64_t tasks_per_p = A0.paired ? 1 : A0.n_tiles;
     if (A0.P * tasks_per_p == 0) return DH_OK;
@@ -1035,6 +1290,19 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     int rc = ensure_attrs(ctx);
     if (rc) return rc;
     const int N = A0.N;
+    {
+        const int max_nopt = A0.paired ? 1 : A0.opt_cap;
+        const bool small_call = max_nopt <= kSmallTile && A0.P * tasks_per_p >= kSmallMinTasks;
+        const bool fusable = (A0.paired || A0.max_group <= kTileMax) &&
+                             fused_lds_bytes(N, A0.opt_cap) <= (size_t)kLdsMax - 4096;
+        // auto: fused while the request is latency-bound (few tables); large requests keep the
+        // two launches, whose table kernel runs at its own occupancy
+        const bool few = A0.P * (A0.paired ? 1 : A0.n_groups) <= kFusedMaxTables;
+        const bool fused = fusable && (ctx->path == DH_PATH_FUSED ||
+                                       (ctx->path == DH_PATH_AUTO && !small_call && few));
+        ctx->last_path = fused ? DH_PATH_FUSED : DH_PATH_SPLIT;
+        if (fused) return launch_fused(ctx, A0, st);
+    }
     const int tpp = A0.paired ? 1 : A0.n_groups;
     const int words = cl_words(A0);
     const size_t per_p =
@@ -1187,6 +1455,16 @@ int dh_ctx_read_stamps(dh_ctx* ctx, unsigned long long* out, int64_t cap, int64_
                       hipMemcpyDeviceToHost));
     return DH_OK;
 }
+
+int dh_ctx_set_path(dh_ctx* ctx, int path) {
+    if (!ctx) return fail(DH_E_ARG, "ctx is null");
+    if (path != DH_PATH_AUTO && path != DH_PATH_SPLIT && path != DH_PATH_FUSED)
+        return fail(DH_E_ARG, "bad path");
+    ctx->path = path;
+    return DH_OK;
+}
+
+int dh_ctx_last_path(dh_ctx* ctx) { return ctx ? ctx->last_path : DH_E_ARG; }
 
 int dh_ctx_set_exact(dh_ctx* ctx, int on) {
     if (!ctx) return fail(DH_E_ARG, "ctx is null");

@@ -24,6 +24,7 @@ PARAM_STRIDE = 16
 MAX_N = 2048
 STRIKE_ABSOLUTE = 0
 STRIKE_PCT_SPOT = 1
+PATH_AUTO, PATH_SPLIT, PATH_FUSED = 0, 1, 2
 
 _dp = C.POINTER(C.c_double)
 _i8p = C.POINTER(C.c_int8)
@@ -40,6 +41,8 @@ SIGNATURES = {
     "dh_ctx_synchronize": (C.c_int, [_vp]),
     "dh_ctx_stream": (_vp, [_vp]),
     "dh_ctx_set_exact": (C.c_int, [_vp, C.c_int]),
+    "dh_ctx_set_path": (C.c_int, [_vp, C.c_int]),
+    "dh_ctx_last_path": (C.c_int, [_vp]),
     "dh_ctx_debug_stamps": (C.c_int, [_vp, C.c_int]),
     "dh_ctx_read_stamps": (C.c_int, [_vp, C.POINTER(C.c_ulonglong), C.c_int64,
                                      C.POINTER(C.c_int64)]),
@@ -139,6 +142,16 @@ class Context:
     def set_exact(self, on: bool):
         """Validation mode: price every option by the per-term reference-order path."""
         _check(load().dh_ctx_set_exact(self._h, 1 if on else 0))
+
+    def set_path(self, path: int):
+        """Request kernels: PATH_AUTO (default), PATH_SPLIT (table + option launches) or
+        PATH_FUSED (one launch per request where every maturity group is one tile)."""
+        _check(load().dh_ctx_set_path(self._h, int(path)))
+
+    @property
+    def last_path(self) -> int:
+        """PATH_FUSED or PATH_SPLIT: the kernels of the last fast-path request (0 before any)."""
+        return int(load().dh_ctx_last_path(self._h))
 
     def debug_stamps(self, on: bool):
         """Diagnostic build only: record per-block phase stamps of the next COS launches."""
@@ -295,4 +308,4 @@ def default_context(device: int | None = None) -> Context:
 
 __all__ = ["Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "PARAM_STRIDE", "MAX_N", "STRIKE_ABSOLUTE",
-           "STRIKE_PCT_SPOT", "LIB_PATH", "SIGNATURES"]
+           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "LIB_PATH", "SIGNATURES"]

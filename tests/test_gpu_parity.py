@@ -433,3 +433,87 @@ def test_small_tile_path_large_call(dh):
     ref_sse = np.sum(((big - mkt) / mkt) ** 2, axis=1)
     assert rel_close(sse, ref_sse, 1e-12, 0).all()
     assert np.array_equal(bad, np.sum(~(big > 0) | ~np.isfinite(big), axis=1))
+
+
+def _with_path(ctx, path, fn):
+    ctx.set_path(path)
+    try:
+        return fn()
+    finally:
+        ctx.set_path(0)
+
+
+@pytest.mark.parametrize("seed,P,M,n_T,N", [
+    (41, 14, 15, 3, 128),        # C1 shape
+    (42, 14, 1024, 32, 256),     # C2 shape
+    (43, 6, 2000, 20, 512),      # C3-like: 100-option groups, N = 512
+    (44, 5, 300, 3, 64),         # 100-option groups, short series
+    (45, 3, 256, 1, 2048),       # one full 256-option tile, longest series
+    (46, 9, 40, 40, 100),        # one option per group, N not a power of two
+])
+def test_fused_equals_split_bitwise(dh, seed, P, M, n_T, N):
+    """The fused single-launch request kernel and the table + option launches compute every
+    value by the same expressions in the same order: prices, loss sums and invalid counts are
+    identical word for word (calls and puts, clamp-widened strikes, price and loss modes), and
+    both match the oracle."""
+    from dhcos import _native
+    params, rec, K, T, call = _surface_case(seed, P=P, M=M, n_T=n_T, N=N)
+    if M >= 40:
+        K[:4] = [3.0, 30.0, 400.0, 5000.0]                    # clamp-widened at short maturities
+        T[:4] = T.min()
+    ctx = _native.default_context()
+    mkt = np.abs(O.price_many(params[0], 100.0, K, T, 0.03, call, N)) + 1e-3
+    surf = _native.Surface(ctx, K, T, call, mkt)
+    res = {}
+    for path in (_native.PATH_SPLIT, _native.PATH_FUSED):
+        pr = _with_path(ctx, path, lambda: surf.price(rec, N))
+        sse, bad, lp = _with_path(ctx, path, lambda: surf.loss_terms(rec, N, want_prices=True))
+        res[path] = (pr, sse, bad, lp)
+    s, f = res[_native.PATH_SPLIT], res[_native.PATH_FUSED]
+    assert np.array_equal(surf.price(rec, N), f[0])
+    # auto: fused for requests of <= 1,024 tables whose groups are single tiles
+    assert ctx.last_path == (_native.PATH_FUSED if P * len(set(T)) <= 1024 else _native.PATH_SPLIT)
+    for a, b in zip(s, f):
+        assert np.array_equal(a, b), np.max(np.abs(np.asarray(a, float) - np.asarray(b, float)))
+    assert np.array_equal(f[0], f[3])
+    for p in range(0, P, max(1, P // 3)):
+        want = O.price_many(params[p], 100.0, K, T, 0.03, call, N)
+        assert rel_close(f[0][p], want, FID_RTOL, BAR_ATOL).all(), np.max(np.abs(f[0][p] - want))
+    pairs = [_with_path(ctx, path, lambda: ctx.price_pairs(np.repeat(rec[:1], 8, 0), K[:8], T[:8],
+                                                           call[:8], N))
+             for path in (_native.PATH_SPLIT, _native.PATH_FUSED)]
+    assert np.array_equal(pairs[0], pairs[1])
+
+
+def test_fused_loss_handoff_back_to_back(dh):
+    """Fused-kernel loss hand-off over 200 back-to-back device launches on one stream whose param
+    sets change every launch, checked against the split path's sums of the same sets."""
+    import torch
+    from dhcos import _native
+    params, rec, K, T, call = _surface_case(47, P=14, M=1024, n_T=32, N=256)
+    ctx = _native.default_context()
+    mkt = np.abs(O.price_many(params[0], 100.0, K, T, 0.03, call, 256)) + 1e-3
+    surf = _native.Surface(ctx, K, T, call, mkt)
+    rs = np.random.RandomState(5)
+    recs = np.repeat(rec[None], 200, 0)
+    recs[:, :, :13] *= 1 + 0.02 * rs.standard_normal((200, 14, 13))
+    d_rec = torch.tensor(recs, dtype=torch.float64, device="cuda")
+    d_sse = torch.empty((200, 14), dtype=torch.float64, device="cuda")
+    d_bad = torch.empty((200, 14), dtype=torch.int32, device="cuda")
+    st = ctx.stream
+    ctx.set_path(_native.PATH_FUSED)
+    try:
+        for i in range(200):
+            surf.loss_dev(d_rec[i].data_ptr(), 14, d_sse[i].data_ptr(), d_bad[i].data_ptr(),
+                          N=256, stream=st)
+        ctx.synchronize()
+    finally:
+        ctx.set_path(0)
+    got_sse, got_bad = d_sse.cpu().numpy(), d_bad.cpu().numpy()
+    ctx.set_path(_native.PATH_SPLIT)
+    try:
+        for i in range(0, 200, 20):
+            sse, bad, _ = surf.loss_terms(recs[i], 256)
+            assert np.array_equal(sse, got_sse[i]) and np.array_equal(bad, got_bad[i]), i
+    finally:
+        ctx.set_path(0)

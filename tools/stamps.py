@@ -27,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--mode", default="loss")
+    ap.add_argument("--path", type=int, default=0, help="0 auto, 1 split, 2 fused")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     opts, S0, r = bench.make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
@@ -35,6 +36,7 @@ def main():
     host = bench.step_params(cal, 2, cfg["starts"], seed=0)
     for _ in range(3):
         surf.loss_terms(host[0], cfg["N"])
+    surf.ctx.set_path(args.path)
     surf.ctx.debug_stamps(True)
     if args.mode == "loss":
         surf.loss_terms(host[1], cfg["N"])
@@ -42,6 +44,17 @@ def main():
         surf.price(host[1], cfg["N"])
     st = surf.ctx.read_stamps().astype(np.int64)
     surf.ctx.debug_stamps(False)
+    if surf.ctx.last_path == 2:          # cos_fused_kernel: stamps 0..5 of every block
+        st = st[st[:, 0] > 0]
+        print(f"{args.config} {args.mode}: fused-kernel blocks {len(st)}")
+        names = ["prologue+stage", "cf+clamp", "consts+rot", "sums", "loss"]
+        for i, nm in enumerate(names):
+            c = st[:, i + 1] - st[:, i]
+            print(f"  {nm:15s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}  "
+                  f"max {c.max():8.0f} cycles")
+        life = st[:, 5] - st[:, 0]
+        print(f"  lifetime median {np.median(life):8.0f}  max {life.max():8.0f}")
+        return
     tb = st[st[:, 4] > 0]
     print(f"{args.config} {args.mode}: table-kernel blocks {len(tb)}")
     for nm, c in zip(["consts", "cf loop", "reduce"], [tb[:, 5] - tb[:, 4], tb[:, 6] - tb[:, 5],
