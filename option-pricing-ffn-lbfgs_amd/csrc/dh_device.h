@@ -61,20 +61,34 @@ __device__ __forceinline__ double flip_sign(double v, int neg) {   // neg: 0 or 
     return __hiloint2double(__double2hiint(v) ^ (neg << 31), __double2loint(v));
 }
 
+// c + z * p as one fp64 FMA with the constant c read from an SGPR pair.  The compiler's own
+// choice for a polynomial step is v_fmac_f64, whose tied accumulator needs a VGPR copy of c (two
+// v_mov_b32 per step, ~30% of a Horner chain's VALU issue); this VOP3 form moves the constant
+// traffic to the scalar unit, which co-issues with other waves' VALU.  Same rounding as fma().
+__device__ __forceinline__ double fma_k(double z, double p, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "v"(p), "s"(c));
+    return r;
+}
+
 __device__ __forceinline__ void dsincos(double x, double* sp, double* cp) {
     const double q = rint(x * 6.36619772367581382433e-01);           // x * 2/pi
     double r = fma(-q, 1.57079632679489655800e+00, x);                 // pi/2, 3 parts
     r = fma(-q, 6.12323399573676588613e-17, r);
     r = fma(-q, -1.49738490485916983089e-33, r);
     const double z = r * r;
-    const double ps = -1.66666666666666324348e-01 +
-        z * (8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 +
-        z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 +
-        z * 1.58969099521155010221e-10))));
+    double ps = fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+    ps = fma_k(z, ps, 2.75573137070700676789e-06);
+    ps = fma_k(z, ps, -1.98412698298579493134e-04);
+    ps = fma_k(z, ps, 8.33333333332248946124e-03);
+    ps = fma_k(z, ps, -1.66666666666666324348e-01);
     const double s = fma(r * z, ps, r);
-    const double pc = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 +
-        z * (2.48015872894767294178e-05 + z * (-2.75573143513906633035e-07 +
-        z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+    double pc = fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+    pc = fma_k(z, pc, -2.75573143513906633035e-07);
+    pc = fma_k(z, pc, 2.48015872894767294178e-05);
+    pc = fma_k(z, pc, -1.38888888888741095749e-03);
+    pc = fma_k(z, pc, 4.16666666666666019037e-02);
+    pc = z * pc;
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double c = w + (((1.0 - w) - hz) + z * pc);
@@ -83,6 +97,29 @@ __device__ __forceinline__ void dsincos(double x, double* sp, double* cp) {
     const bool swap = qi & 1;
     *sp = flip_sign(swap ? c : s, (qi >> 1) & 1);
     *cp = flip_sign(swap ? s : c, ((qi + 1) >> 1) & 1);
+}
+
+// exp(x): restates the ROCm device library's __ocml_exp_f64 operation for operation (same
+// reduction constants, degree-11 polynomial and range clamps, so the same bits), with the
+// polynomial steps in the fma_k form.
+__device__ __forceinline__ double dexp(double x) {
+    const double q = rint(x * 0x1.71547652b82fep+0);                 // x log2(e)
+    double r = fma(q, -0x1.62e42fefa39efp-1, x);                      // x - q ln2 (2 parts)
+    r = fma(q, -0x1.abc9e3b39803fp-56, r);
+    double p = fma(0x1.ade156a5dcb37p-26, r, 0x1.28af3fca7ab0cp-22);
+    p = fma_k(r, p, 0x1.71dee623fde64p-19);
+    p = fma_k(r, p, 0x1.a01997c89e6b0p-16);
+    p = fma_k(r, p, 0x1.a01a014761f6ep-13);
+    p = fma_k(r, p, 0x1.6c16c1852b7b0p-10);
+    p = fma_k(r, p, 0x1.1111111122322p-7);
+    p = fma_k(r, p, 0x1.55555555502a1p-5);
+    p = fma_k(r, p, 0x1.5555555555511p-3);
+    p = fma_k(r, p, 0x1.000000000000bp-1);
+    p = fma(r, p, 1.0);
+    p = fma(r, p, 1.0);
+    double e = ldexp(p, (int)q);
+    e = (x > 1024.0) ? INFINITY : e;
+    return (x < -1075.0) ? 0.0 : e;
 }
 
 __device__ __forceinline__ cplx cexp_(cplx z) {
@@ -139,10 +176,13 @@ __device__ __forceinline__ double dlog(double x) {
     const double f = m - 1.0;
     const double s = f * drcp(2.0 + f);
     const double z = s * s, w = z * z;
-    const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 +
-                      w * 1.531383769920937332e-01));
-    const double t2 = z * (6.666666666666735130e-01 + w * (2.857142874366239149e-01 +
-                      w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    double p1 = fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01);
+    p1 = fma_k(w, p1, 3.999999999940941908e-01);
+    const double t1 = w * p1;
+    double p2 = fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01);
+    p2 = fma_k(w, p2, 2.857142874366239149e-01);
+    p2 = fma_k(w, p2, 6.666666666666735130e-01);
+    const double t2 = z * p2;
     const double R = t2 + t1;
     const double hfsq = 0.5 * f * f;
     const double dk = (double)k;
@@ -154,26 +194,33 @@ __device__ __forceinline__ double dlog(double x) {
 }
 
 // atan2(y, x) in (-pi, pi]: t = min/max in [0, 1]; for t > tan(pi/8) use
-// atan t = pi/4 + atan((t - 1)/(t + 1)); the fdlibm s_atan.c polynomial on |t'| <= tan(pi/8).
+// atan t = pi/4 + atan((t - 1)/(t + 1)) with (t - 1)/(t + 1) = (mn - mx)/(mn + mx), so one
+// reciprocal serves both ranges; the fdlibm s_atan.c polynomial on |t'| <= tan(pi/8).
+// Branch-free (every case is a select the compiler keeps as one): zeros need no special case
+// (the reciprocal's argument is clamped to the smallest normal, so t = 0 for x = y = 0, and the
+// sign bit of x selects pi - a, giving atan2(+-0, -0) = +-pi); the one deviation from libm is
+// x = -0 with y != 0, which returns pi/2 one ulp high.
 __device__ __forceinline__ double datan2(double y, double x) {
     const double ax = fabs(x), ay = fabs(y);
     const double mx = fmax(ax, ay), mn = fmin(ax, ay);
-    const double t = mn * drcp(mx);
-    const bool big = t > 0.41421356237309503;
-    const double tr = big ? (t - 1.0) * drcp(t + 1.0) : t;
+    const bool big = mn > 0.41421356237309503 * mx;
+    const double tr = (big ? mn - mx : mn) * drcp(fmax(big ? mn + mx : mx, 2.2250738585072014e-308));
     const double z = tr * tr, w = z * z;
-    const double s1 = z * (3.33333333333329318027e-01 + w * (1.42857142725034663711e-01 +
-                      w * (9.09088713343650656196e-02 + w * (6.66107313738753120669e-02 +
-                      w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
-    const double s2 = w * (-1.99999999998764832476e-01 + w * (-1.11111104054623557880e-01 +
-                      w * (-7.69187620504482999495e-02 + w * (-5.83357013379057348645e-02 +
-                      w * -3.65315727442169155270e-02))));
+    double p1 = fma(w, 1.62858201153657823623e-02, 4.97687799461593236017e-02);
+    p1 = fma_k(w, p1, 6.66107313738753120669e-02);
+    p1 = fma_k(w, p1, 9.09088713343650656196e-02);
+    p1 = fma_k(w, p1, 1.42857142725034663711e-01);
+    p1 = fma_k(w, p1, 3.33333333333329318027e-01);
+    const double s1 = z * p1;
+    double p2 = fma(w, -3.65315727442169155270e-02, -5.83357013379057348645e-02);
+    p2 = fma_k(w, p2, -7.69187620504482999495e-02);
+    p2 = fma_k(w, p2, -1.11111104054623557880e-01);
+    p2 = fma_k(w, p2, -1.99999999998764832476e-01);
+    const double s2 = w * p2;
     const double at = tr - tr * (s1 + s2);
     double a = big ? 7.85398163397448278999e-01 + (at + 3.06161699786838301793e-17) : at;
     a = (ay > ax) ? (1.57079632679489655800e+00 - a) + 6.12323399573676588613e-17 : a;
-    a = (x < 0.0 || (x == 0.0 && signbit(x) && ay == 0.0))
-            ? (3.14159265358979311600e+00 - a) + 1.22464679914735317720e-16 : a;
-    a = (mx == 0.0 && !(x < 0.0 || signbit(x))) ? 0.0 : a;            // atan2(+-0, +0)
+    a = signbit(x) ? (3.14159265358979311600e+00 - a) + 1.22464679914735317720e-16 : a;
     a = copysign(a, y);
     return (isnan(x) || isnan(y)) ? x + y : a;
 }
@@ -273,7 +320,7 @@ __device__ __forceinline__ void factor_exponent(const FactorC& F, double u, doub
     const cplx bp = {beta.re + dre, beta.im + dim};
     double es, ec;
     dsincos(-dim * tau, &es, &ec);
-    const double em = exp(-dre * tau);
+    const double em = dexp(-dre * tau);
     const cplx e = {em * ec, em * es};
     const cplx D = {bp.re - (bm.re * e.re - bm.im * e.im), bp.im - (bm.re * e.im + bm.im * e.re)};
     const cplx ome = {1.0 - e.re, -e.im};
@@ -312,12 +359,12 @@ __device__ __forceinline__ double cf_phase_re(const CfConsts& C, double u, doubl
     factor_exponent(C.f2, u, tau, E);
     double js, jc;
     dsincos(u * C.muj, &js, &jc);
-    const double jm = exp(-(C.half_sj2 * (u * u)));
+    const double jm = dexp(-(C.half_sj2 * (u * u)));
     E.re += C.lt * (jm * jc - 1.0);
     E.im += C.lt * (jm * js);
     double ps, pc;
     dsincos(E.im - u * a, &ps, &pc);
-    return exp(E.re) * pc;
+    return dexp(E.re) * pc;
 }
 
 // First two cumulants of one factor (double_heston.py:101-118).  Q1: c1 includes r*tau.

@@ -13,12 +13,13 @@
 //   cos_option_kernel<TPT> one task per (p, tile), a tile = <= 256 options of one maturity:
 //     stage the (p, g) table into LDS, expanded to the strike-independent parts of chi_k/psi_k
 //     (k >= 1, double_heston.py:141-158):  u_k = k pi/(b-a),  T2_k = w_k S0/(1+u_k^2),
-//     T3_k = T2_k u_k,  T4_k = w_k/u_k;  per option only two angle sums remain
-//       S2 = sum_k T2_k cos(k th) + T3_k sin(k th),   S4 = sum_k T4_k sin(k th),
-//       th = pi (log(K/S0) - a)/(b - a),   price = e^{-rT} (const + w0 V_0 - e^{xK} S2 + K S4)
-//     computed by G lanes per group of kR options (lane j: k = 1 + j, 1 + j + G, ...), the
-//     angle advanced by complex rotations e^{i G th} with an exact sincos re-anchor every
-//     kAnchor steps, then DPP butterflies.
+//     T6_k = -T2_k/u_k;  per option one angle sum remains
+//       S = sum_k T2_k cos(k th) + T6_k sin(k th),   th = pi (log(K/S0) - a)/(b - a),
+//       price = e^{-rT} (const + w0 V_0 - e^{xK} S)
+//     (the chi and psi parts at the log-strike, -e^{xK}(T2 cos + T2 u sin) + K (w/u) sin, with
+//     K = S0 e^{xK}), computed by G lanes per group of kR options (lane j: k = 1 + j, 1 + j + G,
+//     ...), cos/sin(k th) advanced by the Chebyshev recurrence x_{k+G} = 2 cos(G th) x_k -
+//     x_{k-G} with an exact sincos re-anchor every kAnchor steps, then DPP butterflies.
 //
 //   Options whose [a, b] is widened by the log-strike clamp (double_heston.py:135-137) are
 //   found and priced by the TABLE kernel (it already carries the CF code): per (p, group) it
@@ -194,6 +195,17 @@ __device__ __forceinline__ void table_prologue(const PriceArgs& A, int64_t q, do
 #define DH_OPTION_WAVES 1
 #endif
 
+// CF entries of one table slot (thread t of TPT): k = t, t + TPT, ..., emitted in increasing k
+// (the k-sums' order) as emit(k, u_k, w_k).
+template <int TPT, typename F>
+__device__ __forceinline__ void table_entries(const dh::CfConsts& CC, int t, int N, double piba,
+                                              double T, double a, double scale, F&& emit) {
+    for (int k = t; k < N; k += TPT) {
+        const double u = k * piba;                                   // k pi / (b - a)
+        emit(k, u, dh::cf_phase_re(CC, u, T, a) * scale);
+    }
+}
+
 // Grid: a fixed number of blocks (resident capacity), each owning a contiguous range of tables.
 // Tables are taken in batches of up to kBatch: lane i of wave 0 computes the truncation range and
 // CF constants of table i of the batch (one prologue latency for up to 64 tables), then every
@@ -241,13 +253,11 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             const double K_first = o_first < gn ? option_strike(A, g0 + o_first, S0) : 0.0;
             double* tw = A.table + q * (int64_t)N;
             double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
-            for (int k = t; k < N; k += TPT) {
-                const double u = k * piba;                       // k pi / (b - a)
-                const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+            table_entries<TPT>(CC, t, N, piba, T, a, scale, [&](int k, double u, double w) {
                 tw[k] = w;
                 if (k == 0) {
                     w0 = 0.5 * w;
-                    continue;
+                    return;
                 }
                 // chi_k / psi_k at d = b: u (b - a) = k pi, so cos = (-1)^k and sin = 0 exactly
                 // (the reference evaluates them with ~1e-16 rounding noise; c1 = sum T4 sin(.)
@@ -256,7 +266,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                 const double T2 = w * S0 * dh::drcp(1.0 + u * u);
                 c0 += T2 * eb * cb;
                 c5 += T2 * ea;
-            }
+            });
             for (int off = 1; off < 64; off <<= 1) {
                 c0 += __shfl_xor(c0, off, 64);
                 c1 += __shfl_xor(c1, off, 64);
@@ -340,54 +350,56 @@ struct Consts {
     double c0, c1, c5, w0, a, b, eb, ea;
 };
 
-// sum' of one option from the table constants and its angle sums (k = 0 term:
+// sum' of one option from the table constants and its angle sum (k = 0 term:
 // chi_0 = e^d - e^c, psi_0 = d - c, double_heston.py:142-143,154-155).
 __device__ __forceinline__ double option_sum(const Consts& C, bool is_call, double S0, double K,
-                                             double xK, double exK, double s2, double s4) {
+                                             double xK, double exK, double sum) {
     const double v0 = is_call ? (S0 * (C.eb - exK) - K * (C.b - xK))
                               : (K * (xK - C.a) - S0 * (exK - C.ea));
     const double cst = is_call ? (C.c0 - K * C.c1) : C.c5;
-    return cst + C.w0 * v0 - exK * s2 + K * s4;
+    return cst + C.w0 * v0 - exK * sum;
 }
 
 // Angle sums of up to kR options on lanes k = k1, k1 + G, ...:
-//   s2_j = sum_k T2_k cos(k th_j) + T3_k sin(k th_j),  s4_j = sum_k T4_k sin(k th_j)
-// the angle u_k (xK_j - a) advances by the option's e^{i G th_j} rotation (cs, ss: staged once
-// per option), with an exact sincos re-anchor every kAnchor steps; one (T2, T3) ds_read_b128 and
-// one T4 read serve all kR options.
+//   s_j = sum_k T2_k cos(k th_j) + T6_k sin(k th_j)
+// cos/sin(k th_j) follow the Chebyshev recurrence x_{k+G} = 2 cos(G th_j) x_k - x_{k-G} (two FMAs
+// per option-term; cg, sg = cos/sin(G th_j) staged once per option), re-anchored by an exact sincos
+// every kAnchor steps: a rounding error introduced n steps before an anchor is amplified by at
+// most n, so every cos/sin is within ~kAnchor^2 eps / 2 ~ 2e-13 of exact.  One (T2, T6)
+// ds_read_b128 serves all kR options.
 __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double (&dx)[kR],
-                                             const double (&cs)[kR], const double (&ss)[kR],
-                                             const double* tu, const double2* t23,
-                                             const double* t4, double (&s2)[kR],
-                                             double (&s4)[kR]) {
+                                             const double (&cg)[kR], const double (&sg)[kR],
+                                             const double* tu, const double2* t26,
+                                             double (&sum)[kR]) {
 #pragma unroll
-    for (int j = 0; j < kR; ++j) {
-        s2[j] = 0.0;
-        s4[j] = 0.0;
-    }
+    for (int j = 0; j < kR; ++j) sum[j] = 0.0;
     if (k1 >= N) return;
-    double cx[kR], sx[kR];
-    const double u1 = tu[k1];
+    double cx[kR], sx[kR], cp[kR], sp[kR], c2[kR];
 #pragma unroll
-    for (int j = 0; j < kR; ++j) dh::dsincos(u1 * dx[j], &sx[j], &cx[j]);
-    int n = 0;
+    for (int j = 0; j < kR; ++j) c2[j] = 2.0 * cg[j];
+    int n = kAnchor;
     for (int k = k1; k < N; k += G, ++n) {
-        if (n == kAnchor) {
+        if (n == kAnchor) {                 // exact (k, k - G) pair
             const double uk = tu[k];
 #pragma unroll
-            for (int j = 0; j < kR; ++j) dh::dsincos(uk * dx[j], &sx[j], &cx[j]);
+            for (int j = 0; j < kR; ++j) {
+                dh::dsincos(uk * dx[j], &sx[j], &cx[j]);
+                cp[j] = cx[j] * cg[j] + sx[j] * sg[j];          // cos((k - G) th)
+                sp[j] = sx[j] * cg[j] - cx[j] * sg[j];          // sin((k - G) th)
+            }
             n = 0;
         }
-        const double2 a23 = t23[k];
-        const double a4 = t4[k];
+        const double2 a26 = t26[k];
 #pragma unroll
         for (int j = 0; j < kR; ++j) {
-            s2[j] = fma(a23.x, cx[j], s2[j]);
-            s2[j] = fma(a23.y, sx[j], s2[j]);
-            s4[j] = fma(a4, sx[j], s4[j]);
-            const double cn = cx[j] * cs[j] - sx[j] * ss[j];
-            sx[j] = sx[j] * cs[j] + cx[j] * ss[j];
+            sum[j] = fma(a26.x, cx[j], sum[j]);
+            sum[j] = fma(a26.y, sx[j], sum[j]);
+            const double cn = fma(c2[j], cx[j], -cp[j]);
+            const double sn = fma(c2[j], sx[j], -sp[j]);
+            cp[j] = cx[j];
+            sp[j] = sx[j];
             cx[j] = cn;
+            sx[j] = sn;
         }
     }
 }
@@ -446,15 +458,14 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
 }
 
 __host__ __device__ constexpr int option_lds_doubles(int N, int opt_cap) {
-    // (T2,T3)[N] T4[N] u[N] | K, mkt, sse, bad, xK, e^xK, cos/sin step [opt_cap] |
+    // (T2,T6)[N] u[N] | K, mkt, sse, bad, xK, e^xK, cos/sin step [opt_cap] |
     // call, perm [opt_cap] ints, rounded to whole 16-byte pairs
-    return 4 * N + 8 * opt_cap + ((2 * opt_cap + 3) / 4) * 2;
+    return 3 * N + 8 * opt_cap + ((2 * opt_cap + 3) / 4) * 2;
 }
 
 // LDS view of one staged tile: the expanded (p, g) table and the per-option arrays
 struct TileLds {
-    double2* t23;
-    double* t4;
+    double2* t26;     // (T2_k, T6_k)
     double* tu;
     double* K;
     double* mkt;
@@ -470,10 +481,9 @@ struct TileLds {
 
 __device__ __forceinline__ TileLds tile_lds(double* base, int N, int cap) {
     TileLds L;
-    L.t23 = (double2*)base;
-    L.t4 = base + 2 * N;
-    L.tu = base + 3 * N;
-    L.K = base + 4 * N;
+    L.t26 = (double2*)base;
+    L.tu = base + 2 * N;
+    L.K = base + 3 * N;
     L.mkt = L.K + cap;
     L.sse = L.mkt + cap;
     L.bad = L.sse + cap;
@@ -521,29 +531,25 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
             cs[j] = use[j] ? L.cs[oi] : 1.0;
             ss[j] = use[j] ? sj : 0.0;
         }
-        double s2[kR], s4[kR];
-        angle_sums_r(1 + gl, G, N, dx, cs, ss, L.tu, L.t23, L.t4, s2, s4);
+        double sm[kR];
+        angle_sums_r(1 + gl, G, N, dx, cs, ss, L.tu, L.t26, sm);
         for (int off = 1; off < G; off <<= 1) {
 #pragma unroll
-            for (int j = 0; j < kR; ++j) {
-                s2[j] += __shfl_xor(s2[j], off, 64);
-                s4[j] += __shfl_xor(s4[j], off, 64);
-            }
+            for (int j = 0; j < kR; ++j) sm[j] += __shfl_xor(sm[j], off, 64);
         }
         // every lane of the group holds the (bitwise identical) sums: lane j finalises option j
         if (G >= R) {
-            double m2 = s2[0], m4 = s4[0];
+            double m = sm[0];
             bool mu = use[0];
 #pragma unroll
             for (int j = 1; j < kR; ++j) {
-                m2 = gl == j ? s2[j] : m2;
-                m4 = gl == j ? s4[j] : m4;
+                m = gl == j ? sm[j] : m;
                 mu = gl == j ? use[j] : mu;
             }
             if (gl < R && mu) {
                 const int oi = gi * R + gl;
                 const double sum = option_sum(C, L.call[oi] != 0, S0, L.K[oi], L.xK[oi],
-                                              L.exK[oi], m2, m4);
+                                              L.exK[oi], m);
                 record_price(A, p, L.perm[oi], L.mkt[oi], oi, disc * sum, L.sse, L.bad);
             }
         } else if (gl == 0) {
@@ -552,7 +558,7 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
                 if (!use[j]) continue;
                 const int oi = gi * R + j;
                 const double sum = option_sum(C, L.call[oi] != 0, S0, L.K[oi], L.xK[oi],
-                                              L.exK[oi], s2[j], s4[j]);
+                                              L.exK[oi], sm[j]);
                 record_price(A, p, L.perm[oi], L.mkt[oi], oi, disc * sum, L.sse, L.bad);
             }
         }
@@ -580,8 +586,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
 
     const int cap = A.opt_cap;
     const TileLds L = tile_lds(smem + (size_t)slot * option_lds_doubles(N, cap), N, cap);
-    double2* t23 = L.t23;
-    double* t4 = L.t4;
+    double2* t26 = L.t26;
     double* tu = L.tu;
     double* lK = L.K;
     double* lmkt = L.mkt;
@@ -619,7 +624,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     const double ba = C.b - C.a;
     const double T = active ? A.T[opt0] : 1.0;
     const double disc = exp(-P.r * T);
-    // stage the (p, g) table, expanded to u, (T2, T3), T4 (same expressions as the table
+    // stage the (p, g) table, expanded to u, (T2, T6) (same expressions as the table
     // kernel's k-sums), and per-option data: log(K/S0), e^{xK} and the G-step rotation of each
     // option; clamp-widened options (bit set by the table kernel) are recorded right here
     if (active) {
@@ -629,8 +634,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
             const double w = tw[k];
             const double u = k * piba;
             const double T2 = k == 0 ? 0.0 : w * P.S0 * dh::drcp(1.0 + u * u);
-            t23[k] = make_double2(T2, T2 * u);
-            t4[k] = k == 0 ? 0.0 : w * dh::drcp(u);
+            t26[k] = make_double2(T2, k == 0 ? 0.0 : -(T2 * dh::drcp(u)));
             tu[k] = u;
         }
         const double ustep = G * dh::kPi / ba;
@@ -673,7 +677,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
 // ----------------------------------------------------------------------------------------------
 // option kernel, small tiles (<= kSmallTile options per tile): one lane carries kRs options of a
 // tile through every term k = 1 .. N-1.  Its step rotation e^{i th} is also its start angle, the
-// 8-byte table w_k is read straight from L2/MALL and expanded to (T2, T3, T4) on the fly
+// 8-byte table w_k is read straight from L2/MALL and expanded to (T2, T6) on the fly
 // (amortised over kRs options), and a task's partial is reduced over its L lanes (L = lanes per
 // task, a power of two <= 4) before the same fence-free hand-off.  Per lane this is ~9 VALU
 // instructions per option-term with no LDS, no per-lane anchors and no butterflies -- the
@@ -723,8 +727,9 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
     const unsigned long long* msk = A.cl_mask + q * cl_words(A);
     const double* clp = A.cl_price + q * (int64_t)A.max_group;
 
-    // per option: log-strike, clamp bit, start angle = step rotation e^{i th}
-    double dx[kRs], c[kRs], sn[kRs], cs[kRs], ss[kRs], s2[kRs], s4[kRs];
+    // per option: log-strike, clamp bit; cos/sin(k th) by the Chebyshev recurrence from
+    // (k = 0, k = 1) = (1 + 0i, e^{i th})
+    double dx[kRs], c[kRs], sn[kRs], cp[kRs], sp[kRs], cs[kRs], ss[kRs], sm[kRs];
     bool use[kRs];
     double lsum = 0.0, lbad = 0.0;
 #pragma unroll
@@ -759,31 +764,40 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
         ss[j] = s1;
         c[j] = c1;
         sn[j] = s1;
-        s2[j] = 0.0;
-        s4[j] = 0.0;
+        cp[j] = 1.0;
+        sp[j] = 0.0;
+        sm[j] = 0.0;
     }
     const double* tw = A.table + q * (int64_t)A.N;
+    double c2[kRs];
+#pragma unroll
+    for (int j = 0; j < kRs; ++j) c2[j] = 2.0 * cs[j];
     int n = 0;
     for (int k = 1; k < A.N; ++k, ++n) {
-        if (n == kAnchor) {
+        if (n == kAnchor) {                 // exact (k, k - 1) pair
             const double uk = k * piba;
 #pragma unroll
-            for (int j = 0; j < kRs; ++j) dh::dsincos(uk * dx[j], &sn[j], &c[j]);
+            for (int j = 0; j < kRs; ++j) {
+                dh::dsincos(uk * dx[j], &sn[j], &c[j]);
+                cp[j] = c[j] * cs[j] + sn[j] * ss[j];
+                sp[j] = sn[j] * cs[j] - c[j] * ss[j];
+            }
             n = 0;
         }
         const double w = active ? tw[k] : 0.0;
         const double u = k * piba;
         const double T2 = w * S0 * dh::drcp(1.0 + u * u);
-        const double T3 = T2 * u;
-        const double T4 = w * dh::drcp(u);
+        const double T6 = -(T2 * dh::drcp(u));
 #pragma unroll
         for (int j = 0; j < kRs; ++j) {
-            s2[j] = fma(T2, c[j], s2[j]);
-            s2[j] = fma(T3, sn[j], s2[j]);
-            s4[j] = fma(T4, sn[j], s4[j]);
-            const double cn = c[j] * cs[j] - sn[j] * ss[j];
-            sn[j] = sn[j] * cs[j] + c[j] * ss[j];
+            sm[j] = fma(T2, c[j], sm[j]);
+            sm[j] = fma(T6, sn[j], sm[j]);
+            const double cn = fma(c2[j], c[j], -cp[j]);
+            const double snn = fma(c2[j], sn[j], -sp[j]);
+            cp[j] = c[j];
+            sp[j] = sn[j];
             c[j] = cn;
+            sn[j] = snn;
         }
     }
     // finalise this lane's options, then the task partial over its L lanes (fixed tree)
@@ -794,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
         const double K = option_strike(A, m, S0);
         double ratio;
         const double xK = option_logk(K, S0, ratio);
-        const double sum = option_sum(C, A.call[m] != 0, S0, K, xK, ratio, s2[j], s4[j]);
+        const double sum = option_sum(C, A.call[m] != 0, S0, K, xK, ratio, sm[j]);
         const double price = disc * sum;
         if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
         if (A.part_sse) {
@@ -843,7 +857,7 @@ template <int TPT1>
 __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(PriceArgs A, int tpt2) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ double shc[kTabC];
-    __shared__ double red[4][kBlock / 64];
+    __shared__ double red[4][1];
     __shared__ unsigned long long cmask[kTileMax / 64];
     const int nthr = blockDim.x;
     const int t = threadIdx.x;
@@ -889,43 +903,24 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
 
     const double a = shc[0], b = shc[1], eb = shc[2], ea = shc[3], scale = shc[4], piba = shc[5];
     const double T = shc[24];
-    // ---- CF loop (threads < TPT1, as cos_table_kernel<TPT1>): expanded table into LDS ----
+    // ---- CF loop (threads < TPT1, one entry each up to N = 256): expanded table into LDS ----
+    __shared__ double w0s;
     if (t < TPT1) {
         dh::CfConsts CC;
         {
             double* cc = (double*)&CC;
             for (int j = 0; j < 16; ++j) cc[j] = shc[6 + j];
         }
-        double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
-        for (int k = t; k < N; k += TPT1) {
-            const double u = k * piba;
-            const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+        table_entries<TPT1>(CC, t, N, piba, T, a, scale, [&](int k, double u, double w) {
             L.tu[k] = u;
             if (k == 0) {
-                w0 = 0.5 * w;
-                L.t23[0] = make_double2(0.0, 0.0);
-                L.t4[0] = 0.0;
-                continue;
+                w0s = 0.5 * w;
+                L.t26[0] = make_double2(0.0, 0.0);
+                return;
             }
-            const double cb = (k & 1) ? -1.0 : 1.0;
             const double T2 = w * S0 * dh::drcp(1.0 + u * u);
-            c0 += T2 * eb * cb;
-            c5 += T2 * ea;
-            L.t23[k] = make_double2(T2, T2 * u);
-            L.t4[k] = w * dh::drcp(u);
-        }
-        for (int off = 1; off < 64; off <<= 1) {
-            c0 += __shfl_xor(c0, off, 64);
-            c1 += __shfl_xor(c1, off, 64);
-            c5 += __shfl_xor(c5, off, 64);
-            w0 += __shfl_xor(w0, off, 64);
-        }
-        if (lane == 0) {
-            red[0][wv] = c0;
-            red[1][wv] = c1;
-            red[2][wv] = c5;
-            red[3][wv] = w0;
-        }
+            L.t26[k] = make_double2(T2, -(T2 * dh::drcp(u)));
+        });
     }
     // ---- clamp-widened options (double_heston.py:135-137), decided and priced per wave ----
     for (int base = wv * 64; base < gn; base += nthr) {
@@ -955,22 +950,38 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
     __syncthreads();
     DH_STAMP(A, 2);
 
-    // ---- fixed-order constants (as the table kernel) || per-option rotations ----
-    Consts C;
-    {
-        double sm[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int j = 0; j < 4; ++j)
-            for (int w = 0; w < TPT1 / 64; ++w) sm[j] += red[j][w];
-        C = Consts{sm[0], sm[1], sm[2], sm[3], a, b, eb, ea};
+    // ---- k-sums in the canonical order of a 64-thread table slot (wave 0, from the LDS table;
+    //      the same bits as cos_table_kernel) || per-option rotations ----
+    if (wv == 0) {
+        double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = lane == 0 ? w0s : 0.0;
+        for (int k = lane; k < N; k += 64) {
+            if (k == 0) continue;
+            const double T2 = L.t26[k].x;
+            const double cb = (k & 1) ? -1.0 : 1.0;
+            c0 += T2 * eb * cb;
+            c5 += T2 * ea;
+        }
+        for (int off = 1; off < 64; off <<= 1) {
+            c0 += __shfl_xor(c0, off, 64);
+            c1 += __shfl_xor(c1, off, 64);
+            c5 += __shfl_xor(c5, off, 64);
+            w0 += __shfl_xor(w0, off, 64);
+        }
+        if (lane == 0) {
+            red[0][0] = c0;
+            red[1][0] = c1;
+            red[2][0] = c5;
+            red[3][0] = w0;
+        }
     }
     const double disc = exp(-prm[14] * T);
     const int G = group_lanes(gn, N, tpt2);
     {
-        const double ustep = G * dh::kPi / (C.b - C.a);
+        const double ustep = G * dh::kPi / (b - a);
         for (int i = t; i < gn; i += nthr) {
             const bool cl = (cmask[i >> 6] >> (i & 63)) & 1ull;
             double ss, cs;
-            dh::dsincos(ustep * (cl ? 0.0 : L.xK[i] - C.a), &ss, &cs);
+            dh::dsincos(ustep * (cl ? 0.0 : L.xK[i] - a), &ss, &cs);
             L.cs[i] = cs;
             L.ss[i] = cl ? NAN : ss;
             if (cl) record_price(A, p, L.perm[i], L.mkt[i], i, lclp[i], L.sse, L.bad);
@@ -979,6 +990,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
     __syncthreads();
     DH_STAMP(A, 3);
 
+    const Consts C{0.0 + red[0][0], 0.0 + red[1][0], 0.0 + red[2][0], 0.0 + red[3][0], a, b, eb, ea};
     if (t < tpt2) tile_sums(A, p, C, S0, disc, gn, G, tpt2, t, true, L);
     DH_STAMP(A, 4);
     if (A.part_sse) {
@@ -1137,7 +1149,11 @@ struct DevBuf {
     }
 };
 
-int table_tpt(int N) { return N >= 256 ? 256 : (N >= 128 ? 128 : 64); }
+// Threads per table.  The split path's table kernel always runs 64 (one wave per table, which
+// also defines the canonical order of the per-table k-sums); the fused kernel takes one entry per
+// thread up to N = 256 (latency) and re-forms the k-sums in the 64-lane order from LDS.
+int table_tpt(int) { return 64; }
+int fused_tpt(int N) { return N <= 64 ? 64 : (N <= 128 ? 128 : 256); }
 
 // option-kernel threads per task: enough lanes for ceil(nopt/kR) groups, LDS permitting
 int option_tpt(int max_nopt, int N, int cap) {
@@ -1156,7 +1172,7 @@ struct dh_ctx {
     DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, cl_mask,
         cl_price, aux0, aux1, aux2, aux3;
     bool attr_set = false;
-    int table_resident[3] = {0, 0, 0};   // resident cos_table_kernel<64/128/256> blocks, chip
+    int table_resident = 0;   // resident cos_table_kernel<64> blocks, whole chip
     int exact = 0;          // validation mode: every option through the per-term exact path
     int path = DH_PATH_AUTO;   // fused / split request kernels (dh_ctx_set_path)
     int last_path = 0;         // kernels of the last fast-path request (dh_ctx_last_path)
@@ -1206,13 +1222,10 @@ int ensure_attrs(dh_ctx* ctx) {
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    const void* fns[3] = {(const void*)cos_table_kernel<64>, (const void*)cos_table_kernel<128>,
-                          (const void*)cos_table_kernel<256>};
-    for (int i = 0; i < 3; ++i) {
-        int per_cu = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fns[i], kBlock, 0));
-        ctx->table_resident[i] = std::max(1, per_cu) * std::max(1, cus);
-    }
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)cos_table_kernel<64>,
+                                                         kBlock, 0));
+    ctx->table_resident = std::max(1, per_cu) * std::max(1, cus);
     ctx->attr_set = true;
     return DH_OK;
 }
@@ -1255,7 +1268,7 @@ size_t fused_lds_bytes(int N, int cap) {
 int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     const int N = A0.N;
     const int tpp = A0.paired ? 1 : A0.n_groups;
-    const int t1 = table_tpt(N);
+    const int t1 = fused_tpt(N);
     const int max_nopt = A0.paired ? 1 : A0.opt_cap;
     const int t2 = option_tpt(max_nopt, N, A0.opt_cap);
     const size_t lds = fused_lds_bytes(N, A0.opt_cap);
@@ -1340,17 +1353,13 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         A.cl_price = (double*)ctx->cl_price.ptr;
         A.stamps = ctx->stamps_on ? (unsigned long long*)ctx->stamps.ptr : nullptr;
         const int64_t n_q = A.np * tpp;
-        const int res = ctx->table_resident[t1 == 64 ? 0 : (t1 == 128 ? 1 : 2)];
+        const int res = ctx->table_resident;
         const int64_t b1 = std::min<int64_t>((n_q + kBlock / t1 - 1) / (kBlock / t1), res);
         const int64_t n_t = A.np * tasks_per_p;
         const int64_t b2 = small ? (n_t * L + kBlock - 1) / kBlock
                                  : (n_t + kBlock / t2 - 1) / (kBlock / t2);
         if (b1 > 0x7fffffffLL || b2 > 0x7fffffffLL) return fail(DH_E_ARG, "launch too large");
-        switch (t1) {
-            case 64: hipLaunchKernelGGL(cos_table_kernel<64>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
-            case 128: hipLaunchKernelGGL(cos_table_kernel<128>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
-            default: hipLaunchKernelGGL(cos_table_kernel<256>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
-        }
+        hipLaunchKernelGGL(cos_table_kernel<64>, dim3((unsigned)b1), dim3(kBlock), 0, st, A);
         HIP_TRY(hipGetLastError());
         if (small) {
             hipLaunchKernelGGL(cos_option_small_kernel, dim3((unsigned)b2), dim3(kBlock), 0, st, A, L);
