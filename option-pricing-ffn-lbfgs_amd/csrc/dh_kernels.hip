@@ -373,33 +373,48 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
                                              double (&sum)[kR]) {
 #pragma unroll
     for (int j = 0; j < kR; ++j) sum[j] = 0.0;
-    if (k1 >= N) return;
-    double cx[kR], sx[kR], cp[kR], sp[kR], c2[kR];
+    double c2[kR];
 #pragma unroll
     for (int j = 0; j < kR; ++j) c2[j] = 2.0 * cg[j];
-    int n = kAnchor;
-    for (int k = k1; k < N; k += G, ++n) {
-        if (n == kAnchor) {                 // exact (k, k - G) pair
-            const double uk = tu[k];
-#pragma unroll
-            for (int j = 0; j < kR; ++j) {
-                dh::dsincos(uk * dx[j], &sx[j], &cx[j]);
-                cp[j] = cx[j] * cg[j] + sx[j] * sg[j];          // cos((k - G) th)
-                sp[j] = sx[j] * cg[j] - cx[j] * sg[j];          // sin((k - G) th)
-            }
-            n = 0;
-        }
-        const double2 a26 = t26[k];
+    // segments of kAnchor steps, each opened by an exact (k, k - G) pair; inside a segment two
+    // steps per iteration, so x_k and x_{k-G} swap registers instead of being copied, with the
+    // next table entry read ahead of the arithmetic that needs it
+    for (int k0 = k1; k0 < N; k0 += kAnchor * G) {
+        double cx[kR], sx[kR], cp[kR], sp[kR];
+        const double uk = tu[k0];
 #pragma unroll
         for (int j = 0; j < kR; ++j) {
-            sum[j] = fma(a26.x, cx[j], sum[j]);
-            sum[j] = fma(a26.y, sx[j], sum[j]);
-            const double cn = fma(c2[j], cx[j], -cp[j]);
-            const double sn = fma(c2[j], sx[j], -sp[j]);
-            cp[j] = cx[j];
-            sp[j] = sx[j];
-            cx[j] = cn;
-            sx[j] = sn;
+            dh::dsincos(uk * dx[j], &sx[j], &cx[j]);
+            cp[j] = cx[j] * cg[j] + sx[j] * sg[j];              // cos((k - G) th)
+            sp[j] = sx[j] * cg[j] - cx[j] * sg[j];              // sin((k - G) th)
+        }
+        const int kend = min(N, k0 + kAnchor * G);
+        int k = k0;
+        double2 ta = t26[k];
+        for (; k + G < kend; k += 2 * G) {
+            const double2 tb = t26[k + G];
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {                      // step k: x_{k+G} into (cp, sp)
+                sum[j] = fma(ta.x, cx[j], sum[j]);
+                sum[j] = fma(ta.y, sx[j], sum[j]);
+                cp[j] = fma(c2[j], cx[j], -cp[j]);
+                sp[j] = fma(c2[j], sx[j], -sp[j]);
+            }
+            ta = t26[min(k + 2 * G, N - 1)];
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {                      // step k + G: x_{k+2G} into (cx, sx)
+                sum[j] = fma(tb.x, cp[j], sum[j]);
+                sum[j] = fma(tb.y, sp[j], sum[j]);
+                cx[j] = fma(c2[j], cp[j], -cx[j]);
+                sx[j] = fma(c2[j], sp[j], -sx[j]);
+            }
+        }
+        if (k < kend) {
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {
+                sum[j] = fma(ta.x, cx[j], sum[j]);
+                sum[j] = fma(ta.y, sx[j], sum[j]);
+            }
         }
     }
 }
@@ -772,32 +787,51 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
     double c2[kRs];
 #pragma unroll
     for (int j = 0; j < kRs; ++j) c2[j] = 2.0 * cs[j];
-    int n = 0;
-    for (int k = 1; k < A.N; ++k, ++n) {
-        if (n == kAnchor) {                 // exact (k, k - 1) pair
-            const double uk = k * piba;
+    // segments of kAnchor terms (the first starts exact at k = 1; later ones re-anchor on an
+    // exact (k, k - 1) pair), two terms per iteration with x_k / x_{k-1} swapping registers
+    const int N = A.N;
+    for (int k0 = 1; k0 < N; k0 += kAnchor) {
+        if (k0 > 1) {
+            const double uk = k0 * piba;
 #pragma unroll
             for (int j = 0; j < kRs; ++j) {
                 dh::dsincos(uk * dx[j], &sn[j], &c[j]);
                 cp[j] = c[j] * cs[j] + sn[j] * ss[j];
                 sp[j] = sn[j] * cs[j] - c[j] * ss[j];
             }
-            n = 0;
         }
-        const double w = active ? tw[k] : 0.0;
-        const double u = k * piba;
-        const double T2 = w * S0 * dh::drcp(1.0 + u * u);
-        const double T6 = -(T2 * dh::drcp(u));
+        const int kend = min(N, k0 + kAnchor);
+        int k = k0;
+        double wa = active ? tw[k] : 0.0;
+        for (; k + 1 < kend; k += 2) {
+            const double wb = active ? tw[k + 1] : 0.0;
+            const double ua = k * piba, ub = (k + 1) * piba;
+            const double T2a = wa * S0 * dh::drcp(1.0 + ua * ua);
+            const double T6a = -(T2a * dh::drcp(ua));
+            const double T2b = wb * S0 * dh::drcp(1.0 + ub * ub);
+            const double T6b = -(T2b * dh::drcp(ub));
+            wa = active ? tw[min(k + 2, N - 1)] : 0.0;
 #pragma unroll
-        for (int j = 0; j < kRs; ++j) {
-            sm[j] = fma(T2, c[j], sm[j]);
-            sm[j] = fma(T6, sn[j], sm[j]);
-            const double cn = fma(c2[j], c[j], -cp[j]);
-            const double snn = fma(c2[j], sn[j], -sp[j]);
-            cp[j] = c[j];
-            sp[j] = sn[j];
-            c[j] = cn;
-            sn[j] = snn;
+            for (int j = 0; j < kRs; ++j) {
+                sm[j] = fma(T2a, c[j], sm[j]);
+                sm[j] = fma(T6a, sn[j], sm[j]);
+                cp[j] = fma(c2[j], c[j], -cp[j]);               // x_{k+1}
+                sp[j] = fma(c2[j], sn[j], -sp[j]);
+                sm[j] = fma(T2b, cp[j], sm[j]);
+                sm[j] = fma(T6b, sp[j], sm[j]);
+                c[j] = fma(c2[j], cp[j], -c[j]);                // x_{k+2}
+                sn[j] = fma(c2[j], sp[j], -sn[j]);
+            }
+        }
+        if (k < kend) {
+            const double u = k * piba;
+            const double T2 = wa * S0 * dh::drcp(1.0 + u * u);
+            const double T6 = -(T2 * dh::drcp(u));
+#pragma unroll
+            for (int j = 0; j < kRs; ++j) {
+                sm[j] = fma(T2, c[j], sm[j]);
+                sm[j] = fma(T6, sn[j], sm[j]);
+            }
         }
     }
     // finalise this lane's options, then the task partial over its L lanes (fixed tree)
