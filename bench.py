@@ -88,23 +88,60 @@ def step_params(cal, n_steps, starts, seed):
     return out
 
 
-def cpu_baseline(cal_opts, S0, r, N, budget_s=12.0):
-    """Scalar-structured NumPy port (oracle/) of the reference pricer, 1 core, bounded sample."""
+def _cpu_worker(args):
+    """One CPU process of the baseline: price options of the workload one by one with the
+    scalar-structured NumPy port for budget_s seconds (strided start so workers differ)."""
+    opts, prm, S0, r, N, budget_s, start = args
     from oracle import dh_oracle as O
-    x = DoubleHestonJumpCalibrator(S0, r, cal_opts).get_initial_guess(0)
-    prm = O.to_params(x)
     n, t0 = 0, time.perf_counter()
     with np.errstate(all="ignore"):
         while True:
-            o = cal_opts[(n * 37) % len(cal_opts)]
+            o = opts[(start + n * 37) % len(opts)]
             O.price_scalar(prm, S0, o["strike"], o["maturity"], r, o["option_type"] == "call", N)
             n += 1
             if time.perf_counter() - t0 > budget_s and n >= 16:
                 break
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "option-prices/s", "cores": 1, "kind": "port",
-            "sample": f"{n} options of the workload surface priced one by one at N={N} by "
-                      f"oracle.dh_oracle.price_scalar (reference algorithm restated) in {dt:.1f} s"}
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline(cal_opts, S0, r, N, budget_s=12.0, cores=None):
+    """Scalar-structured NumPy port (oracle/) of the reference pricer on `cores` host processes
+    (default: 16, the GPU box's CPU share), each on a bounded sample of the
+    workload's options.  Must run before this process touches the GPU: the pool forks."""
+    import multiprocessing as mp
+    from oracle import dh_oracle as O
+    cores = int(cores or min(16, os.cpu_count() or 1))
+    x = DoubleHestonJumpCalibrator(S0, r, cal_opts).get_initial_guess(0)
+    prm = O.to_params(x)
+    jobs = [(cal_opts, prm, S0, r, N, budget_s, 101 * i) for i in range(cores)]
+    if cores == 1:
+        res = [_cpu_worker(jobs[0])]
+    else:
+        with mp.get_context("fork").Pool(cores) as pool:
+            res = pool.map(_cpu_worker, jobs)
+    n = sum(c for c, _ in res)
+    rate = sum(c / t for c, t in res)
+    wall = max(t for _, t in res)
+    return {"value": rate, "unit": "option-prices/s", "cores": cores, "kind": "port",
+            "per_core": rate / cores,
+            "sample": f"{n} options of the workload priced one by one at N={N} by "
+                      f"oracle.dh_oracle.price_scalar (reference algorithm restated) in "
+                      f"{cores} processes x {wall:.1f} s"}
+
+
+def cpu_options(cfg):
+    """The workload's option list, built without the GPU (for the CPU baseline)."""
+    if cfg.get("gen"):
+        Krel = np.tile(np.linspace(80.0, 120.0, 8), 4)
+        T = np.repeat([0.25, 0.5, 1.0, 2.0], 8)
+        return [{"strike": float(k), "maturity": float(t), "option_type": "call", "price": 1.0}
+                for k, t in zip(Krel, T)], 100.0, 0.03
+    S0, r = 100.0, 0.03
+    kk, tt = np.meshgrid(np.linspace(0.8, 1.2, cfg["nK"]) * S0, np.linspace(0.1, 2.0, cfg["nT"]))
+    K, T = kk.ravel(), tt.ravel()
+    call = np.ones(K.size, dtype=bool) if not cfg["put_itm"] else (K >= S0)
+    return [{"strike": float(k), "maturity": float(t), "price": 1.0,
+             "option_type": "call" if c else "put"} for k, t, c in zip(K, T, call)], S0, r
 
 
 def kernel_label(ctx):
@@ -140,7 +177,7 @@ CONFIGS = {
 }
 
 
-def bench_generator(args, cfg, world, rank, dev, coll, stream):
+def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
     """C5: one step = price every (param set, option) of a 1M-sample generator batch
     (dh_surface_price_dev, strikes K_relative * spot / 100 formed on the device)."""
     sptr = stream.cuda_stream
@@ -221,11 +258,9 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream):
                            "cos_terms": N, "prices_per_step": P * M,
                            "parallelism": f"independent batches per rank x{world}"},
                 "roofline": roofline}
-        if not args.no_cpu:
-            opts = [{"strike": float(k), "maturity": float(t), "option_type": "call", "price": 1.0}
-                    for k, t in zip(Krel, T)]
-            line["cpu_baseline"] = cpu_baseline(opts, 100.0, 0.03, N, args.cpu_budget)
-            line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+        if cpu:
+            line["cpu_baseline"] = cpu
+            line["speedup_vs_cpu"] = value / cpu["value"]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -246,11 +281,19 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N > 1 "
                          "with several ranks on one GPU)")
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="CPU-baseline processes (default min(16, os.cpu_count()))")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # CPU baseline first, on rank 0 at N = 1 only, before anything initialises the GPU (its
+    # process pool forks)
+    cpu = None
+    if not args.no_cpu and rank == 0 and world == 1:
+        c_opts, c_S0, c_r = cpu_options(cfg)
+        cpu = cpu_baseline(c_opts, c_S0, c_r, cfg["N"], args.cpu_budget, args.cpu_cores)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, torch.cuda.device_count())     # == LOCAL_RANK on a full node
     if world > 1:
@@ -270,7 +313,7 @@ def main():
     sptr = stream.cuda_stream
     assert sptr, "expected a non-default HIP stream"
     if cfg.get("gen"):
-        return bench_generator(args, cfg, world, rank, dev, coll, stream)
+        return bench_generator(args, cfg, world, rank, dev, coll, stream, cpu)
 
     opts, S0, r = make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
     M = len(opts)
@@ -394,9 +437,9 @@ def main():
         }
         if calib:
             line["calibration"] = calib
-        if not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(opts, S0, r, N, args.cpu_budget)
-            line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+        if cpu:
+            line["cpu_baseline"] = cpu
+            line["speedup_vs_cpu"] = value / cpu["value"]
             if calib and world == 1:
                 # the same calibration on the CPU port: every loss evaluation prices M options
                 cpu_s = calib["loss_evals_rank0"] * M / line["cpu_baseline"]["value"]

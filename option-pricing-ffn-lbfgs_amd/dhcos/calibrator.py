@@ -14,6 +14,11 @@ What changes relative to the reference, and what does not:
     start's 14 points share one launch (S = 14 x starts param sets).
   * Starts are independent, so the per-start trajectory does not depend on how many starts share
     a launch; the best start is chosen with the reference's strict ``<`` in start order.
+  * SciPy's optimizer itself is driven through its reverse-communication entry point
+    (``scipy.optimize._lbfgsb.setulb``) by ``lbfgsb_steps``, a line-for-line restatement of
+    ``_minimize_lbfgsb``'s loop for jac=True and no bounds: one Python thread advances every
+    start, so a lockstep iteration costs one launch plus the setulb calls, with no thread
+    hand-offs.  Same setulb inputs in the same order, so the same trajectory as ``minimize``.
 """
 from __future__ import annotations
 
@@ -23,7 +28,8 @@ from dataclasses import dataclass
 from typing import Dict, List
 
 import numpy as np
-from scipy.optimize import minimize
+from scipy.optimize import OptimizeResult, _lbfgsb, minimize
+from scipy.optimize._lbfgsb_py import status_messages, task_messages
 
 from . import _native
 from .pricer import resolve_call
@@ -89,17 +95,28 @@ def fd_request_points(x0, h=FD_ABS_STEP):
     """The points SciPy 1.15 evaluates for one function+gradient request with jac=None:
     x0 and x0 + h_i e_i, plus dx_i = (x0_i + h_i) - x0_i.  h_i falls back to the relative step
     sqrt(eps) * sign(x0_i) * max(1, |x0_i|) where the absolute step vanishes."""
-    x0 = np.asarray(x0, dtype=np.float64).ravel()
-    n = x0.size
-    sign = (x0 >= 0).astype(float) * 2 - 1
-    hv = np.full(n, float(h))
-    hv = np.where(((x0 + hv) - x0) == 0,
-                  np.sqrt(np.finfo(np.float64).eps) * sign * np.maximum(1.0, np.abs(x0)), hv)
-    X = np.repeat(x0[None, :], n + 1, axis=0)
+    X, dx = fd_request_points_many(np.asarray(x0, dtype=np.float64).reshape(1, -1), h)
+    return X, dx[0]
+
+
+_SQRT_EPS = float(np.sqrt(np.finfo(np.float64).eps))
+
+
+def fd_request_points_many(X0, h=FD_ABS_STEP):
+    """fd_request_points for every row of X0 [S, n]: -> X [S * (n + 1), n] (per start x0 then
+    x0 + h_i e_i, start-major) and dx [S, n].  Elementwise the same arithmetic."""
+    X0 = np.asarray(X0, dtype=np.float64)
+    S, n = X0.shape
+    hv = np.full((S, n), float(h))
+    vanish = ((X0 + hv) - X0) == 0
+    if vanish.any():
+        sign = (X0 >= 0).astype(float) * 2 - 1
+        hv[vanish] = (_SQRT_EPS * sign * np.maximum(1.0, np.abs(X0)))[vanish]
+    X = np.repeat(X0[:, None, :], n + 1, axis=1)
     idx = np.arange(n)
-    X[idx + 1, idx] += hv
-    dx = X[idx + 1, idx] - x0
-    return X, dx
+    X[:, idx + 1, idx] += hv
+    dx = X[:, idx + 1, idx] - X0
+    return X.reshape(S * (n + 1), n), dx
 
 
 class DoubleHestonJumpCalibrator:
@@ -275,8 +292,81 @@ class DoubleHestonJumpCalibrator:
 
 
 # ----------------------------------------------------------------------------------------------
-# lockstep multi-start driver
+# L-BFGS-B through SciPy's reverse-communication interface
 # ----------------------------------------------------------------------------------------------
+def lbfgsb_steps(x0, maxiter, maxfun, m=10, ftol=1e-9, gtol=1e-6, maxls=20):
+    """Generator restating ``scipy.optimize._lbfgsb_py._minimize_lbfgsb`` (SciPy 1.15.3, the
+    ``while True`` loop around ``_lbfgsb.setulb``) for ``jac=True`` and no bounds, with the
+    objective evaluated by the caller: it yields the point x at which it needs (f, g) and
+    receives them through ``send``; its return value (``StopIteration.value``) is the
+    OptimizeResult.  The evaluation bookkeeping is ``ScalarFunction``'s
+    (scipy/optimize/_differentiable_functions.py): x0 is evaluated at construction (nfev = 1)
+    and a point is re-evaluated only when it differs from the last one (``np.array_equal``)."""
+    factr = ftol / np.finfo(float).eps
+    pgtol = gtol
+    x0 = np.asarray(x0).ravel()
+    n = x0.size
+    sf_x = x0.astype(np.float64)                     # ScalarFunction.__init__: f and g at x0
+    sf_f, sf_g = yield sf_x
+    nfev = 1
+    nbd = np.zeros(n, np.int32)
+    low_bnd = np.zeros(n, np.float64)
+    upper_bnd = np.zeros(n, np.float64)
+    x = np.array(x0, dtype=np.float64)
+    f = np.array(0.0, dtype=np.int32)
+    g = np.zeros((n,), dtype=np.int32)
+    wa = np.zeros(2 * m * n + 5 * n + 11 * m * m + 8 * m, np.float64)
+    iwa = np.zeros(3 * n, dtype=np.int32)
+    task = np.zeros(2, dtype=np.int32)
+    ln_task = np.zeros(2, dtype=np.int32)
+    lsave = np.zeros(4, dtype=np.int32)
+    isave = np.zeros(44, dtype=np.int32)
+    dsave = np.zeros(29, dtype=np.float64)
+    n_iterations = 0
+    while True:
+        g = g.astype(np.float64)
+        _lbfgsb.setulb(m, x, low_bnd, upper_bnd, nbd, f, g, factr, pgtol, wa, iwa, task, lsave,
+                       isave, dsave, maxls, ln_task)
+        if task[0] == 3:
+            if not np.array_equal(x, sf_x):          # ScalarFunction.fun_and_grad
+                sf_x = x.astype(np.float64)
+                sf_f, sf_g = yield sf_x
+                nfev += 1
+            f, g = sf_f, sf_g
+        elif task[0] == 1:
+            n_iterations += 1
+            if n_iterations >= maxiter:
+                task[0] = 5
+                task[1] = 504
+            elif nfev > maxfun:
+                task[0] = 5
+                task[1] = 502
+        else:
+            break
+    if task[0] == 4:
+        warnflag = 0
+    elif nfev > maxfun or n_iterations >= maxiter:
+        warnflag = 1
+    else:
+        warnflag = 2
+    msg = status_messages[task[0]] + ": " + task_messages[task[1]]
+    return OptimizeResult(fun=f, jac=g, nfev=nfev, njev=nfev, nit=n_iterations,
+                          status=warnflag, message=msg, x=x, success=(warnflag == 0))
+
+
+# jac=True: nfev counts one per request, SciPy's FD path counts 14 -> rescale maxfun so the
+# `nfev > maxfun` stop fires at the same request (scipy/_lbfgsb_py.py:466-469)
+_MAXFUN = SCIPY_MAXFUN // (N_PARAMS + 1)
+
+
+def _minimize_start(fun, x0, maxiter):
+    """``minimize(method='L-BFGS-B', jac=True)`` with the reference's options (kept as the
+    independent cross-check of ``lbfgsb_steps`` in the tests)."""
+    return minimize(fun=fun, x0=x0, method="L-BFGS-B", jac=True,
+                    options={"maxiter": maxiter, "ftol": 1e-9, "gtol": 1e-6,
+                             "maxfun": _MAXFUN})
+
+
 class _StartState:
     """Per-start bookkeeping that mirrors the reference's per-start resets (:253-254)."""
 
@@ -285,109 +375,54 @@ class _StartState:
         self.best_loss = np.inf
 
 
-class _Lockstep:
-    """Collects the function+gradient requests of all live starts and serves them with one
-    launch.  Each start runs SciPy's minimize in its own thread; the last thread to arrive
-    evaluates the whole batch.  A start's values depend only on its own x, so results equal the
-    sequential run bit for bit."""
-
-    def __init__(self, cal: DoubleHestonJumpCalibrator, n: int):
-        self.cal = cal
-        self.live = n
-        self.pending = {}
-        self.results = {}
-        self.cv = threading.Condition()
-        self.states = [_StartState() for _ in range(n)]
-        self.launches = 0
-
-    def _run_batch(self):
-        ids = sorted(self.pending)
-        pts = [fd_request_points(self.pending[i]) for i in ids]
-        X = np.concatenate([p[0] for p in pts])
-        try:
-            f = self.cal.loss_batch(X, track=False)
-            self.launches += 1
-            for j, sid in enumerate(ids):
-                fj = f[j * (N_PARAMS + 1):(j + 1) * (N_PARAMS + 1)]
-                st = self.states[sid]
-                st.n_calls += N_PARAMS + 1
-                ok = fj[fj != INVALID_LOSS]
-                if ok.size:
-                    lo = np.min(np.where(np.isnan(ok), np.inf, ok))
-                    if lo < st.best_loss:
-                        st.best_loss = lo
-                self.results[sid] = (fj[0], (fj[1:] - fj[0]) / pts[j][1])
-        except BaseException as e:  # hand the failure to every waiting start
-            for sid in ids:
-                self.results[sid] = e
-        self.pending.clear()
-        self.cv.notify_all()
-
-    def request(self, sid, x):
-        with self.cv:
-            self.pending[sid] = np.array(x, dtype=np.float64)
-            if len(self.pending) >= self.live:
-                self._run_batch()
-            while sid not in self.results:
-                self.cv.wait()
-            r = self.results.pop(sid)
-        if isinstance(r, BaseException):
-            raise r
-        return r
-
-    def finish(self):
-        with self.cv:
-            self.live -= 1
-            if self.pending and len(self.pending) >= self.live:
-                self._run_batch()
-
-
-def _minimize_start(fun, x0, maxiter):
-    # jac=True: nfev counts one per request, SciPy's FD path counts 14 -> rescale maxfun so the
-    # `nfev > maxfun` stop fires at the same request (scipy/_lbfgsb_py.py:466-469)
-    return minimize(fun=fun, x0=x0, method="L-BFGS-B", jac=True,
-                    options={"maxiter": maxiter, "ftol": 1e-9, "gtol": 1e-6,
-                             "maxfun": SCIPY_MAXFUN // (N_PARAMS + 1)})
-
-
 def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: bool = True):
-    """Run one L-BFGS-B per x0; returns [(OptimizeResult, t_done) | None] in start order."""
+    """Run one L-BFGS-B per x0; returns [(OptimizeResult, t_done) | None] in start order.
+
+    lockstep: every live start's function+gradient request shares one launch (S = 14 x live
+    starts); otherwise the starts run one after the other.  A start's values depend only on its
+    own x (the kernels are batch-composition invariant), so both give the same results."""
     n = len(x0s)
     outcomes = [None] * n
     if n == 0:
         return outcomes
-    if not lockstep or n == 1:
-        for s, x0 in enumerate(x0s):
-            cal.n_calls, cal.best_loss = 0, np.inf
+    gens = [lbfgsb_steps(x0, maxiter, _MAXFUN) for x0 in x0s]
+    states = [_StartState() for _ in range(n)]
+    launches = 0
+    order = [list(range(n))] if lockstep else [[s] for s in range(n)]
+    for group in order:
+        pending = {}
+        for sid in group:
+            pending[sid] = next(gens[sid])
+        while pending:
+            ids = sorted(pending)
+            X, dx = fd_request_points_many(np.stack([pending[sid] for sid in ids]))
             try:
-                res = _minimize_start(cal.compute_loss_and_grad, x0, maxiter)
-                outcomes[s] = (res, time.time())
+                f = cal.loss_batch(X, track=False)
             except _native.NativeError:
                 raise
-            except Exception:
-                outcomes[s] = None
-        return outcomes
-    ls = _Lockstep(cal, n)
-    errors = [None] * n
-
-    def worker(s):
-        try:
-            res = _minimize_start(lambda x: ls.request(s, x), x0s[s], maxiter)
-            outcomes[s] = (res, time.time())
-        except BaseException as e:  # noqa: BLE001 -- reference: except -> continue
-            errors[s] = e
-        finally:
-            ls.finish()
-
-    threads = [threading.Thread(target=worker, args=(s,), daemon=True) for s in range(n)]
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
-    for e in errors:
-        if isinstance(e, _native.NativeError):
-            raise e
-    last = ls.states[-1]
+            except Exception:          # reference: except -> continue (the start is dropped)
+                for sid in ids:
+                    gens[sid].close()
+                pending.clear()
+                break
+            launches += 1
+            F = f.reshape(len(ids), N_PARAMS + 1)
+            G = (F[:, 1:] - F[:, :1]) / dx
+            # per-start best valid loss (NaN never wins, 1e10 is not a valid loss)
+            lows = np.min(np.where((F == INVALID_LOSS) | np.isnan(F), np.inf, F), axis=1)
+            for j, sid in enumerate(ids):
+                st = states[sid]
+                st.n_calls += N_PARAMS + 1
+                if lows[j] < st.best_loss:
+                    st.best_loss = lows[j]
+                try:
+                    pending[sid] = gens[sid].send((F[j, 0], G[j]))
+                except StopIteration as stop:
+                    outcomes[sid] = (stop.value, time.time())
+                    del pending[sid]
+                except Exception:      # noqa: BLE001 -- reference: except -> continue
+                    del pending[sid]
+    last = states[-1]
     cal.n_calls, cal.best_loss = last.n_calls, last.best_loss   # state after the last start
-    cal.lockstep_launches = ls.launches
+    cal.lockstep_launches = launches
     return outcomes
