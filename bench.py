@@ -151,14 +151,31 @@ def kernel_label(ctx):
     return "cos_table_kernel + cos_option[_small]_kernel"
 
 
-def pmc_traffic(config):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary."""
+def _pmc(config):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
-            return json.load(fh).get(config, {}).get("hbm_bytes_per_launch")
+            return json.load(fh).get(config, {})
     except (OSError, ValueError):
+        return {}
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary."""
+    return _pmc(config).get("hbm_bytes_per_launch")
+
+
+def pmc_executed(config, ker_ms, launches=1):
+    """Executed fp64 flops of one request (rocprofv3 SQ_INSTS_VALU_*_F64 of its kernels, committed
+    under profiles/) over this run's request time: the hardware rate, beside the convention-based
+    `achieved` (whose per-entry / per-term counts are frozen)."""
+    ks = _pmc(config).get("kernels", {})
+    fl = [k.get("exec_fp64_flop") for k in ks.values()]
+    if not fl or any(f is None for f in fl):
         return None
+    tf = sum(fl) * launches / (ker_ms * 1e-3) / 1e12
+    return {"exec_fp64_flop_per_request": sum(fl) * launches, "TFLOPs": round(tf, 3),
+            "frac": round(tf / PEAK_FP64_TFLOPS, 4), "source": f"profiles/pmc_traffic.json [{config}]"}
 
 
 CONFIGS = {
@@ -244,6 +261,7 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
                 "traffic": tr * n_chunks if tr else None, "launch_pairs": n_chunks,
                 "kernel": kernel_label(surf.ctx) + " (all chunks of one batch, HIP events)",
                 "kernel_ms": round(ker_ms, 4), "flop_per_launch": flop,
+                "executed": pmc_executed(args.config, ker_ms, n_chunks),
                 "alg_bytes_per_launch": alg_bytes,
                 "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
                         "peak_GBs": PEAK_HBM_GBS,
@@ -389,6 +407,7 @@ def main():
                 "traffic": pmc_traffic(args.config),
                 "kernel": kernel_label(surf.ctx) + " (one request, HIP events)",
                 "kernel_ms": round(ker_ms, 5), "flop_per_launch": flop,
+                "executed": pmc_executed(args.config, ker_ms),
                 "alg_bytes_per_launch": alg_bytes,
                 "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
                         "peak_GBs": PEAK_HBM_GBS,

@@ -8,7 +8,9 @@ committed evidence under profiles/:
 
 HBM bytes follow MI355X_MICROARCH.md's rocprofv3 section: FETCH_SIZE and WRITE_SIZE come from
 separate passes and are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide coalesced
-read, so it is doubled.  A request is one cos_table_kernel + one cos_option_kernel launch.
+read, so it is doubled.  A request is one cos_fused_kernel launch (latency-bound requests) or one
+cos_table_kernel + one option-kernel launch (large requests): whichever the config spends its
+time in.
 
 usage: python tools/summarize_profiles.py --tag r01 [--src gpurun_out/prof]
 """
@@ -21,7 +23,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel")
+KERNELS = ("cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel")
 
 
 def short(name):
@@ -48,8 +50,10 @@ def main():
     tpath = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     md = [f"# Profile summary {args.tag}", "",
-          "One request = cos_table_kernel + the option kernel (cos_option_kernel, or cos_option_small_kernel for large calls on <=16-option tiles). Durations: rocprofv3 --kernel-trace "
-          "--stats average; counters: per-launch medians of separate --pmc passes.", ""]
+          "One request = cos_fused_kernel (requests of <= 1,024 tables), or cos_table_kernel + the "
+          "option kernel (cos_option_kernel, or cos_option_small_kernel for large calls on "
+          "<=16-option tiles). Durations: rocprofv3 --kernel-trace --stats average; counters: "
+          "per-launch medians of separate --pmc passes.", ""]
     for c in args.configs.split(","):
         stats = os.path.join(args.src, f"{args.tag}_{c}_stats_kernel_stats.csv")
         if not os.path.exists(stats):
@@ -62,10 +66,14 @@ def main():
             if k:
                 avg[k] = float(r["AverageNs"])
                 total[k] = float(r["TotalDurationNs"])
-        # the request's option kernel: whichever option-kernel variant this config spends its
-        # time in (the other one only serves the bench's small spot-check call)
-        opt = max((k for k in KERNELS[1:] if k in total), key=lambda k: total[k])
-        req_kernels = ("cos_table_kernel", opt)
+        # the request's kernels: the fused kernel if the config spends its time there, else the
+        # table kernel + whichever option-kernel variant dominates (the others only serve the
+        # bench's small spot-check calls)
+        if total.get("cos_fused_kernel", 0.0) >= max(total.values()):
+            req_kernels = ("cos_fused_kernel",)
+        else:
+            opt = max((k for k in KERNELS[2:] if k in total), key=lambda k: total[k])
+            req_kernels = ("cos_table_kernel", opt)
         vals = collections.defaultdict(list)
         for f in glob.glob(os.path.join(args.src, f"{args.tag}_{c}_pmc*_counter_collection.csv")):
             for r in csv.DictReader(open(f)):
@@ -104,7 +112,7 @@ def main():
         req_ns = sum(per_kernel[k]["avg_ns"] or 0.0 for k in req_kernels)
         traffic[c] = {"round": args.tag, "hbm_bytes_per_launch": hbm, "request_avg_ns": req_ns,
                       "kernels": per_kernel,
-                      "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->bytes, both kernels"}
+                      "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->bytes, the request's kernels"}
         md += [f"## {c}", "", "| kernel | avg us | fetch MB | write MB | exec fp64 GFLOP | "
                "exec fp64 TFLOP/s | wait_any/wave_cycles |", "|---|---|---|---|---|---|---|"]
         for k in req_kernels:
