@@ -304,7 +304,10 @@ __device__ __forceinline__ FactorC factor_consts(double v0, double kap, double t
     return F;
 }
 
-__device__ __forceinline__ void factor_exponent(const FactorC& F, double u, double tau, cplx& E) {
+// One factor's contribution X to the exponent E: kappa theta / sigma^2 ((beta - d) tau - 2 log Q)
+// + B v0.  E = ((D + X1) + X2) + J with D = (0, drift u) and J the jump part, in that order in every
+// path, so every path agrees.
+__device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau) {
     const cplx beta = {F.kap, -(F.rs * u)};
     const double s2u = F.s2 * u;
     const cplx dd = {fma(beta.re, beta.re, -beta.im * beta.im) + s2u * u,
@@ -329,8 +332,8 @@ __device__ __forceinline__ void factor_exponent(const FactorC& F, double u, doub
     const cplx Q = cdiv_rcp(D, {2.0 * dre, 2.0 * dim});
     const double lq_re = 0.5 * dlog(fma(Q.re, Q.re, Q.im * Q.im));
     const double lq_im = datan2(Q.im, Q.re);
-    E.re += F.coef * (bm.re * tau - 2.0 * lq_re) + B.re * F.v0;
-    E.im += F.coef * (bm.im * tau - 2.0 * lq_im) + B.im * F.v0;
+    return {F.coef * (bm.re * tau - 2.0 * lq_re) + B.re * F.v0,
+            F.coef * (bm.im * tau - 2.0 * lq_im) + B.im * F.v0};
 }
 
 // Per-(param set, T) constants of the fast CF.
@@ -352,19 +355,31 @@ __device__ __forceinline__ CfConsts cf_consts(const Params& P, double tau) {
     return C;
 }
 
-// Re(phi(u) e^{-i u a}) via the exponent form.
-__device__ __forceinline__ double cf_phase_re(const CfConsts& C, double u, double tau, double a) {
-    cplx E = {0.0, C.drift * u};
-    factor_exponent(C.f1, u, tau, E);
-    factor_exponent(C.f2, u, tau, E);
+// jump part J of the exponent: lambda tau (e^{i u mu - sj^2 u^2 / 2} - 1)  (double_heston.py:93)
+__device__ __forceinline__ cplx jump_x(const CfConsts& C, double u) {
     double js, jc;
     dsincos(u * C.muj, &js, &jc);
     const double jm = dexp(-(C.half_sj2 * (u * u)));
-    E.re += C.lt * (jm * jc - 1.0);
-    E.im += C.lt * (jm * js);
+    return {C.lt * (jm * jc - 1.0), C.lt * (jm * js)};
+}
+
+// Re(phi(u) e^{-i u a}) = e^{Re E} cos(Im E - u a) from the exponent's parts.
+__device__ __forceinline__ double cf_phase_from(const CfConsts& C, double u, double a, cplx X1,
+                                                cplx X2, cplx J) {
+    cplx E = {0.0, C.drift * u};
+    E = cadd(E, X1);
+    E = cadd(E, X2);
+    E = cadd(E, J);
     double ps, pc;
     dsincos(E.im - u * a, &ps, &pc);
     return dexp(E.re) * pc;
+}
+
+// Re(phi(u) e^{-i u a}) via the exponent form, one lane per entry.
+__device__ __forceinline__ double cf_phase_re(const CfConsts& C, double u, double tau, double a) {
+    const cplx X1 = factor_x(C.f1, u, tau);
+    const cplx X2 = factor_x(C.f2, u, tau);
+    return cf_phase_from(C, u, a, X1, X2, jump_x(C, u));
 }
 
 // First two cumulants of one factor (double_heston.py:101-118).  Q1: c1 includes r*tau.

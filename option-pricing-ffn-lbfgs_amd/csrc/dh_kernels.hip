@@ -937,7 +937,9 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
 
     const double a = shc[0], b = shc[1], eb = shc[2], ea = shc[3], scale = shc[4], piba = shc[5];
     const double T = shc[24];
-    // ---- CF loop (threads < TPT1, one entry each up to N = 256): expanded table into LDS ----
+    // ---- CF loop (threads < TPT1, one entry each up to N = 256): expanded table into LDS.
+    //      (A lane pair per entry, one Heston factor each, cut C1 by 5% but cost C2 2%: the CF
+    //      phase of a C2 request is issue-bound on the CUs that host two blocks.) ----
     __shared__ double w0s;
     if (t < TPT1) {
         dh::CfConsts CC;
@@ -1012,7 +1014,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
     const int G = group_lanes(gn, N, tpt2);
     {
         const double ustep = G * dh::kPi / (b - a);
-        for (int i = t; i < gn; i += nthr) {
+        for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {          // wave 0 does the sums
             const bool cl = (cmask[i >> 6] >> (i & 63)) & 1ull;
             double ss, cs;
             dh::dsincos(ustep * (cl ? 0.0 : L.xK[i] - a), &ss, &cs);
