@@ -10,6 +10,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "dh_sincos_table.h"
+
 namespace dh {
 
 constexpr double kPi = 3.141592653589793;  // np.pi
@@ -97,6 +99,29 @@ __device__ __forceinline__ void dsincos(double x, double* sp, double* cp) {
     const bool swap = qi & 1;
     *sp = flip_sign(swap ? c : s, (qi >> 1) & 1);
     *cp = flip_sign(swap ? s : c, ((qi + 1) >> 1) & 1);
+}
+
+// sin and cos by a 128-entry table (the CF loop's form): x = q pi/64 + r with |r| <= pi/128 (the
+// 3-part FMA Cody-Waite reduction of dsincos scaled by 2^-5, exact), sin/cos(q pi/64) from an LDS
+// copy of kSinCosPi64 (one ds_read_b128; correctly rounded entries), sin r and cos r by Taylor
+// polynomials through r^7 / r^8 (the next terms are < 1e-18 relative), then the angle-addition
+// formulas.  ~1 ulp for |x| < 2^20; 17 VALU instructions against dsincos's 41.
+__device__ __forceinline__ void dsincos_t(double x, const double2* __restrict__ tab, double* sp,
+                                          double* cp) {
+    const double q = rint(x * 20.371832715762604);                    // x * 64/pi
+    double r = fma(-q, 0.04908738521234052, x);                        // pi/64, 3 parts
+    r = fma(-q, 1.9135106236677394e-18, r);
+    r = fma(-q, -4.6793278276849057e-35, r);
+    const double2 sc = tab[(int)q & 127];                              // sin, cos (q pi/64)
+    const double z = r * r;
+    double ps = fma(z, -0.0001984126984126984, 0.008333333333333333);
+    ps = fma_k(z, ps, -0.16666666666666666);
+    const double sr = fma(r * z, ps, r);                               // sin r
+    double pc = fma(z, 2.48015873015873e-05, -0.001388888888888889);
+    pc = fma_k(z, pc, 0.041666666666666664);
+    const double cr = fma(z * z, pc, fma(z, -0.5, 1.0));               // cos r
+    *sp = fma(sc.x, cr, sc.y * sr);
+    *cp = fma(sc.y, cr, -(sc.x * sr));
 }
 
 // exp(x): restates the ROCm device library's __ocml_exp_f64 operation for operation (same
@@ -307,7 +332,8 @@ __device__ __forceinline__ FactorC factor_consts(double v0, double kap, double t
 // One factor's contribution X to the exponent E: kappa theta / sigma^2 ((beta - d) tau - 2 log Q)
 // + B v0.  E = ((D + X1) + X2) + J with D = (0, drift u) and J the jump part, in that order in every
 // path, so every path agrees.
-__device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau) {
+__device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau,
+                                         const double2* __restrict__ sct) {
     const cplx beta = {F.kap, -(F.rs * u)};
     const double s2u = F.s2 * u;
     const cplx dd = {fma(beta.re, beta.re, -beta.im * beta.im) + s2u * u,
@@ -322,7 +348,7 @@ __device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau)
     const cplx bm = {beta.re - dre, beta.im - dim};
     const cplx bp = {beta.re + dre, beta.im + dim};
     double es, ec;
-    dsincos(-dim * tau, &es, &ec);
+    dsincos_t(-dim * tau, sct, &es, &ec);
     const double em = dexp(-dre * tau);
     const cplx e = {em * ec, em * es};
     const cplx D = {bp.re - (bm.re * e.re - bm.im * e.im), bp.im - (bm.re * e.im + bm.im * e.re)};
@@ -356,30 +382,39 @@ __device__ __forceinline__ CfConsts cf_consts(const Params& P, double tau) {
 }
 
 // jump part J of the exponent: lambda tau (e^{i u mu - sj^2 u^2 / 2} - 1)  (double_heston.py:93)
-__device__ __forceinline__ cplx jump_x(const CfConsts& C, double u) {
+__device__ __forceinline__ cplx jump_x(const CfConsts& C, double u,
+                                       const double2* __restrict__ sct) {
     double js, jc;
-    dsincos(u * C.muj, &js, &jc);
+    dsincos_t(u * C.muj, sct, &js, &jc);
     const double jm = dexp(-(C.half_sj2 * (u * u)));
     return {C.lt * (jm * jc - 1.0), C.lt * (jm * js)};
 }
 
 // Re(phi(u) e^{-i u a}) = e^{Re E} cos(Im E - u a) from the exponent's parts.
 __device__ __forceinline__ double cf_phase_from(const CfConsts& C, double u, double a, cplx X1,
-                                                cplx X2, cplx J) {
+                                                cplx X2, cplx J, const double2* __restrict__ sct) {
     cplx E = {0.0, C.drift * u};
     E = cadd(E, X1);
     E = cadd(E, X2);
     E = cadd(E, J);
     double ps, pc;
-    dsincos(E.im - u * a, &ps, &pc);
+    dsincos_t(E.im - u * a, sct, &ps, &pc);
     return dexp(E.re) * pc;
 }
 
-// Re(phi(u) e^{-i u a}) via the exponent form, one lane per entry.
-__device__ __forceinline__ double cf_phase_re(const CfConsts& C, double u, double tau, double a) {
-    const cplx X1 = factor_x(C.f1, u, tau);
-    const cplx X2 = factor_x(C.f2, u, tau);
-    return cf_phase_from(C, u, a, X1, X2, jump_x(C, u));
+// Re(phi(u) e^{-i u a}) via the exponent form, one lane per entry; sct = LDS copy of kSinCosPi64
+// (load_sincos_table).
+__device__ __forceinline__ double cf_phase_re(const CfConsts& C, double u, double tau, double a,
+                                              const double2* __restrict__ sct) {
+    const cplx X1 = factor_x(C.f1, u, tau, sct);
+    const cplx X2 = factor_x(C.f2, u, tau, sct);
+    return cf_phase_from(C, u, a, X1, X2, jump_x(C, u, sct), sct);
+}
+
+// Block-wide copy of the sin/cos table into LDS (the caller synchronises before use).
+__device__ __forceinline__ void load_sincos_table(double2* sct) {
+    for (int i = threadIdx.x; i < 128; i += blockDim.x)
+        sct[i] = make_double2(kSinCosPi64[2 * i], kSinCosPi64[2 * i + 1]);
 }
 
 // First two cumulants of one factor (double_heston.py:101-118).  Q1: c1 includes r*tau.

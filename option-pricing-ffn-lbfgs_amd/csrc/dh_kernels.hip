@@ -131,14 +131,14 @@ __device__ __forceinline__ double option_strike(const PriceArgs& A, int m, doubl
 // the sum' over k = k_first, k_first + k_step, ...
 __device__ __forceinline__ double clamped_term_sum(const Params& P, double T, double K, double xK,
                                                    double a, double b, bool is_call, int k_first,
-                                                   int k_step, int N) {
+                                                   int k_step, int N, const double2* sct) {
     const dh::CfConsts CC = dh::cf_consts(P, T);
     const double ba = b - a;
     const double scale = 2.0 / ba;
     double acc = 0.0;
     for (int k = k_first; k < N; k += k_step) {
         const double u = k * dh::kPi / ba;
-        const double w = dh::cf_phase_re(CC, u, T, a) * scale;
+        const double w = dh::cf_phase_re(CC, u, T, a, sct) * scale;
         double chi, psi;
         if (is_call) dh::cos_coeffs(k, xK, b, a, b, chi, psi);
         else dh::cos_coeffs(k, a, xK, a, b, chi, psi);
@@ -199,10 +199,11 @@ __device__ __forceinline__ void table_prologue(const PriceArgs& A, int64_t q, do
 // (the k-sums' order) as emit(k, u_k, w_k).
 template <int TPT, typename F>
 __device__ __forceinline__ void table_entries(const dh::CfConsts& CC, int t, int N, double piba,
-                                              double T, double a, double scale, F&& emit) {
+                                              double T, double a, double scale,
+                                              const double2* sct, F&& emit) {
     for (int k = t; k < N; k += TPT) {
         const double u = k * piba;                                   // k pi / (b - a)
-        emit(k, u, dh::cf_phase_re(CC, u, T, a) * scale);
+        emit(k, u, dh::cf_phase_re(CC, u, T, a, sct) * scale);
     }
 }
 
@@ -219,6 +220,8 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
     constexpr int kWaves = TPT / 64;         // waves per slot
     __shared__ double shc[kBatch][kTabC];
     __shared__ double red[kBatch][4][kWaves];
+    __shared__ double2 sct[128];
+    dh::load_sincos_table(sct);           // synchronised by the first batch's barrier
     const int slot = __builtin_amdgcn_readfirstlane(threadIdx.x / TPT);
     const int t = threadIdx.x % TPT;
     const int lane = threadIdx.x & 63;
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             const double K_first = o_first < gn ? option_strike(A, g0 + o_first, S0) : 0.0;
             double* tw = A.table + q * (int64_t)N;
             double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
-            table_entries<TPT>(CC, t, N, piba, T, a, scale, [&](int k, double u, double w) {
+            table_entries<TPT>(CC, t, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
                 tw[k] = w;
                 if (k == 0) {
                     w0 = 0.5 * w;
@@ -313,7 +316,8 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                     const int m = g0 + base + l;
                     const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
                     const double bc = (x + 0.1 > b) ? x + 0.1 : b;
-                    double v = clamped_term_sum(P, T, Kl, x, ac, bc, A.call[m] != 0, lane, 64, N);
+                    double v = clamped_term_sum(P, T, Kl, x, ac, bc, A.call[m] != 0, lane, 64, N,
+                                                sct);
                     for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
                     if (lane == 0) A.cl_price[slot0 + base + l] = disc * v;
                 }
@@ -892,6 +896,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ double shc[kTabC];
     __shared__ double red[4][1];
+    __shared__ double2 sct[128];
     __shared__ unsigned long long cmask[kTileMax / 64];
     const int nthr = blockDim.x;
     const int t = threadIdx.x;
@@ -920,6 +925,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
 
     // ---- prologue (thread 0) || per-option staging (wave 0 takes the last indices) ----
     if (t == 0) table_prologue(A, q, shc);
+    dh::load_sincos_table(sct);
     for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
         const int m = g0 + i;
         const double K = option_strike(A, m, S0);
@@ -947,7 +953,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
             double* cc = (double*)&CC;
             for (int j = 0; j < 16; ++j) cc[j] = shc[6 + j];
         }
-        table_entries<TPT1>(CC, t, N, piba, T, a, scale, [&](int k, double u, double w) {
+        table_entries<TPT1>(CC, t, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
             L.tu[k] = u;
             if (k == 0) {
                 w0s = 0.5 * w;
@@ -978,7 +984,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
             const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
             const double bc = (x + 0.1 > b) ? x + 0.1 : b;
             double v = clamped_term_sum(P, T, L.K[base + l], x, ac, bc, L.call[base + l] != 0,
-                                        lane, 64, N);
+                                        lane, 64, N, sct);
             for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
             if (lane == 0) lclp[base + l] = disc * v;
         }

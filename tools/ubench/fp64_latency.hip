@@ -46,12 +46,15 @@ __global__ void lat(double* out, long long* cyc, double seed) {
 __global__ void cf_lat(const double* prm, double* out, long long* cyc, int ilp) {
     const dh::Params P = dh::load_params(prm);
     const dh::CfConsts C = dh::cf_consts(P, 1.0);
+    __shared__ double2 sct[128];
+    dh::load_sincos_table(sct);
+    __syncthreads();
     double u = 1.0 + threadIdx.x * 1e-3, u2 = 2.0 + threadIdx.x * 1e-3;
     long long t0 = clock64();
     for (int i = 0; i < 32; ++i) {
-        const double w = dh::cf_phase_re(C, u, 1.0, -1.0);
+        const double w = dh::cf_phase_re(C, u, 1.0, -1.0, sct);
         u = 1.0 + 0.1 * w;
-        if (ilp > 1) { const double w2 = dh::cf_phase_re(C, u2, 1.0, -1.0); u2 = 2.0 + 0.1 * w2; }
+        if (ilp > 1) { const double w2 = dh::cf_phase_re(C, u2, 1.0, -1.0, sct); u2 = 2.0 + 0.1 * w2; }
     }
     long long t1 = clock64();
     out[threadIdx.x] = u + u2;
