@@ -65,13 +65,22 @@ __device__ __forceinline__ double flip_sign(double v, int neg) {   // neg: 0 or 
 
 // c + z * p as one fp64 FMA with the constant c read from an SGPR pair.  The compiler's own
 // choice for a polynomial step is v_fmac_f64, whose tied accumulator needs a VGPR copy of c (two
-// v_mov_b32 per step, ~30% of a Horner chain's VALU issue); this VOP3 form moves the constant
-// traffic to the scalar unit, which co-issues with other waves' VALU.  Same rounding as fma().
-__device__ __forceinline__ double fma_k(double z, double p, double c) {
+// v_mov_b32 per step, ~30% of a Horner chain's VALU issue).  Here the constant is written into a
+// fixed, clobbered SGPR pair (s[96:97]) by two s_mov_b32 inside the same asm statement, then
+// read by a VOP3 v_fma_f64: the constant traffic is scalar (it co-issues with other waves' VALU),
+// and since each step materialises its own constant the compiler has nothing to hoist -- hoisted
+// constants had exhausted the SGPR file and been spilled to VGPR lanes (v_writelane /
+// v_readlane, ~5% of the CF loop's VALU).  Same rounding as fma().
+template <unsigned long long B>
+__device__ __forceinline__ double fma_kc(double z, double p) {
     double r;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "v"(p), "s"(c));
+    asm("s_mov_b32 s96, %3\n\ts_mov_b32 s97, %4\n\tv_fma_f64 %0, %1, %2, s[96:97]"
+        : "=v"(r)
+        : "v"(z), "v"(p), "i"((unsigned)(B & 0xffffffffull)), "i"((unsigned)(B >> 32))
+        : "s96", "s97");
     return r;
 }
+#define fma_k(z, p, c) fma_kc<__builtin_bit_cast(unsigned long long, (double)(c))>((z), (p))
 
 __device__ __forceinline__ void dsincos(double x, double* sp, double* cp) {
     const double q = rint(x * 6.36619772367581382433e-01);           // x * 2/pi
@@ -147,6 +156,26 @@ __device__ __forceinline__ double dexp(double x) {
     return (x < -1075.0) ? 0.0 : e;
 }
 
+// dexp for x <= 0 (or -inf / NaN): the same bits without the overflow select (the CF's
+// e^{-Re(d) tau} and Gaussian jump factor e^{-sj^2 u^2 / 2}).
+__device__ __forceinline__ double dexp_nonpos(double x) {
+    const double q = rint(x * 0x1.71547652b82fep+0);
+    double r = fma(q, -0x1.62e42fefa39efp-1, x);
+    r = fma(q, -0x1.abc9e3b39803fp-56, r);
+    double p = fma(0x1.ade156a5dcb37p-26, r, 0x1.28af3fca7ab0cp-22);
+    p = fma_k(r, p, 0x1.71dee623fde64p-19);
+    p = fma_k(r, p, 0x1.a01997c89e6b0p-16);
+    p = fma_k(r, p, 0x1.a01a014761f6ep-13);
+    p = fma_k(r, p, 0x1.6c16c1852b7b0p-10);
+    p = fma_k(r, p, 0x1.1111111122322p-7);
+    p = fma_k(r, p, 0x1.55555555502a1p-5);
+    p = fma_k(r, p, 0x1.5555555555511p-3);
+    p = fma_k(r, p, 0x1.000000000000bp-1);
+    p = fma(r, p, 1.0);
+    p = fma(r, p, 1.0);
+    return (x < -1075.0) ? 0.0 : ldexp(p, (int)q);
+}
+
 __device__ __forceinline__ cplx cexp_(cplx z) {
     double s, c;
     dsincos(z.im, &s, &c);
@@ -189,6 +218,19 @@ __device__ __forceinline__ double dsqrt(double x) {
     double s, r;
     dsqrt_rsqrt(x, s, r);
     return s;
+}
+
+// The same for x finite and > 0 (the CF's |dd|^2 and (|dd| + |Re dd|)/2: dd = beta^2 +
+// sigma^2 u (u + i) is never 0 for kappa, sigma > 0), without the 0 / inf special case.
+__device__ __forceinline__ void dsqrt_rsqrt_pos(double x, double& sq, double& rs) {
+    const double y0 = __builtin_amdgcn_rsq(x);
+    double g = x * y0, h = 0.5 * y0;
+    const double r = fma(-g, h, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    const double d = fma(-g, g, x);
+    sq = fma(h, d, g);
+    rs = 2.0 * h;
 }
 
 // log(x): fdlibm e_log.c, x = 2^k (1 + f), sqrt(1/2) <= 1 + f < sqrt(2), s = f / (2 + f).
@@ -339,9 +381,9 @@ __device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau,
     const cplx dd = {fma(beta.re, beta.re, -beta.im * beta.im) + s2u * u,
                      2.0 * beta.re * beta.im + s2u};
     // principal sqrt: |dd|, then sqrt((|dd| + |Re|)/2) and its reciprocal (no division)
-    const double h = dsqrt(fma(dd.re, dd.re, dd.im * dd.im));
-    double sq, rs;
-    dsqrt_rsqrt(0.5 * (h + fabs(dd.re)), sq, rs);
+    double h, rh, sq, rs;
+    dsqrt_rsqrt_pos(fma(dd.re, dd.re, dd.im * dd.im), h, rh);
+    dsqrt_rsqrt_pos(0.5 * (h + fabs(dd.re)), sq, rs);
     const double other = 0.5 * dd.im * rs;
     const double dre = dd.re > 0.0 ? sq : fabs(other);
     const double dim = dd.re > 0.0 ? other : copysign(sq, dd.im);
@@ -349,7 +391,7 @@ __device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau,
     const cplx bp = {beta.re + dre, beta.im + dim};
     double es, ec;
     dsincos_t(-dim * tau, sct, &es, &ec);
-    const double em = dexp(-dre * tau);
+    const double em = dexp_nonpos(-dre * tau);
     const cplx e = {em * ec, em * es};
     const cplx D = {bp.re - (bm.re * e.re - bm.im * e.im), bp.im - (bm.re * e.im + bm.im * e.re)};
     const cplx ome = {1.0 - e.re, -e.im};
@@ -386,7 +428,7 @@ __device__ __forceinline__ cplx jump_x(const CfConsts& C, double u,
                                        const double2* __restrict__ sct) {
     double js, jc;
     dsincos_t(u * C.muj, sct, &js, &jc);
-    const double jm = dexp(-(C.half_sj2 * (u * u)));
+    const double jm = dexp_nonpos(-(C.half_sj2 * (u * u)));
     return {C.lt * (jm * jc - 1.0), C.lt * (jm * js)};
 }
 

@@ -214,12 +214,17 @@ __device__ __forceinline__ void table_entries(const dh::CfConsts& CC, int t, int
 // finished in a fixed order at the end of the batch (bitwise independent of the grid).
 constexpr int kBatch = 64;
 
+// Slots of TPT = 64 form the per-table k-sums in registers, in the canonical order (lane l of the
+// slot accumulates k = l, l + 64, ... then an xor butterfly); wider slots (fewer, fatter work
+// units when a request has few tables per slot) store T2_k in LDS and let the slot's first wave
+// re-form the same sums in the same order, so every slot width gives the same bits.
 template <int TPT>
 __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(PriceArgs A) {
     constexpr int kTabs = kBlock / TPT;      // table slots per block
-    constexpr int kWaves = TPT / 64;         // waves per slot
+    extern __shared__ __attribute__((aligned(16))) double t2s[];   // TPT > 64: [kTabs][N] T2_k
     __shared__ double shc[kBatch][kTabC];
-    __shared__ double red[kBatch][4][kWaves];
+    __shared__ double red[kBatch][4];
+    __shared__ double w0s[kTabs];
     __shared__ double2 sct[128];
     dh::load_sincos_table(sct);           // synchronised by the first batch's barrier
     const int slot = __builtin_amdgcn_readfirstlane(threadIdx.x / TPT);
@@ -240,47 +245,69 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
         __syncthreads();
         if (b0 == q_begin) DH_STAMP(A, 5);
 
-        for (int i = slot; i < nb; i += kTabs) {
+        for (int i0 = 0; i0 < nb; i0 += kTabs) {        // every thread runs every pass (barriers)
+            const int i = i0 + slot;
+            const bool has = i < nb;
             const int64_t q = b0 + i;
-            const double* c = shc[i];
+            const double* c = shc[has ? i : 0];
             const double a = c[0], b = c[1], eb = c[2], ea = c[3], scale = c[4], piba = c[5];
-            dh::CfConsts CC;
-            {
-                double* cc = (double*)&CC;
-                for (int j = 0; j < 16; ++j) cc[j] = c[6 + j];
-            }
             const double S0 = c[22], T = c[24], lo = c[25], hi = c[26];
-            const int g0 = (int)c[27], gn = (int)c[28];
-            // strike of this lane's first clamp-scan option, loaded now, used after the CF loop
-            const int o_first = wv * 64 + lane;
-            const double K_first = o_first < gn ? option_strike(A, g0 + o_first, S0) : 0.0;
-            double* tw = A.table + q * (int64_t)N;
+            const int g0 = (int)c[27], gn = has ? (int)c[28] : 0;
+            double* t2 = t2s + (TPT > 64 ? slot * N : 0);
             double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
-            table_entries<TPT>(CC, t, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
-                tw[k] = w;
-                if (k == 0) {
-                    w0 = 0.5 * w;
-                    return;
+            if (has) {
+                dh::CfConsts CC;
+                {
+                    double* cc = (double*)&CC;
+                    for (int j = 0; j < 16; ++j) cc[j] = c[6 + j];
                 }
-                // chi_k / psi_k at d = b: u (b - a) = k pi, so cos = (-1)^k and sin = 0 exactly
-                // (the reference evaluates them with ~1e-16 rounding noise; c1 = sum T4 sin(.)
-                // is therefore 0 and kept only for the consts layout)
-                const double cb = (k & 1) ? -1.0 : 1.0;
-                const double T2 = w * S0 * dh::drcp(1.0 + u * u);
-                c0 += T2 * eb * cb;
-                c5 += T2 * ea;
-            });
-            for (int off = 1; off < 64; off <<= 1) {
-                c0 += __shfl_xor(c0, off, 64);
-                c1 += __shfl_xor(c1, off, 64);
-                c5 += __shfl_xor(c5, off, 64);
-                w0 += __shfl_xor(w0, off, 64);
+                double* tw = A.table + q * (int64_t)N;
+                table_entries<TPT>(CC, t, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
+                    tw[k] = w;
+                    if (k == 0) {
+                        w0 = 0.5 * w;
+                        return;
+                    }
+                    // chi_k / psi_k at d = b: u (b - a) = k pi, so cos = (-1)^k and sin = 0
+                    // exactly (the reference evaluates them with ~1e-16 rounding noise; c1 =
+                    // sum T4 sin(.) is therefore 0 and kept only for the consts layout)
+                    const double cb = (k & 1) ? -1.0 : 1.0;
+                    const double T2 = w * S0 * dh::drcp(1.0 + u * u);
+                    if (TPT == 64) {
+                        c0 += T2 * eb * cb;
+                        c5 += T2 * ea;
+                    } else {
+                        t2[k] = T2;
+                    }
+                });
             }
-            if (lane == 0) {
-                red[i][0][wv] = c0;
-                red[i][1][wv] = c1;
-                red[i][2][wv] = c5;
-                red[i][3][wv] = w0;
+            if (TPT > 64) {
+                if (has && t == 0) w0s[slot] = w0;
+                __syncthreads();
+                if (has && wv == 0) {                          // the canonical 64-lane order
+                    w0 = lane == 0 ? w0s[slot] : 0.0;
+                    for (int k = lane; k < N; k += 64) {
+                        if (k == 0) continue;
+                        const double T2 = t2[k];
+                        const double cb = (k & 1) ? -1.0 : 1.0;
+                        c0 += T2 * eb * cb;
+                        c5 += T2 * ea;
+                    }
+                }
+            }
+            if (has && wv == 0) {
+                for (int off = 1; off < 64; off <<= 1) {
+                    c0 += __shfl_xor(c0, off, 64);
+                    c1 += __shfl_xor(c1, off, 64);
+                    c5 += __shfl_xor(c5, off, 64);
+                    w0 += __shfl_xor(w0, off, 64);
+                }
+                if (lane == 0) {
+                    red[i][0] = c0;
+                    red[i][1] = c1;
+                    red[i][2] = c5;
+                    red[i][3] = w0;
+                }
             }
 
             // ---- clamp-widened options of this table's group (double_heston.py:135-137) ----
@@ -289,12 +316,12 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             // k).  Mask words are written for every option, prices only for clamped ones; the
             // option kernel trusts these bits, so the two kernels never disagree on a decision.
             const int64_t slot0 = q * (int64_t)A.max_group;
-            for (int base = wv * 64; base < gn; base += kWaves * 64) {
+            for (int base = wv * 64; base < gn; base += TPT) {
                 const int o = base + lane;
                 bool cl = false;
                 double xK = 0.0, K = 0.0;
                 if (o < gn) {
-                    K = base == wv * 64 ? K_first : option_strike(A, g0 + o, S0);
+                    K = option_strike(A, g0 + o, S0);
                     const double rq = K / S0;
                     if (!(rq >= lo && rq <= hi)) {                   // near or past an edge
                         double ratio;
@@ -322,6 +349,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                     if (lane == 0) A.cl_price[slot0 + base + l] = disc * v;
                 }
             }
+            if (TPT > 64) __syncthreads();                     // t2s / w0s are reused
         }
         __syncthreads();
         if (b0 == q_begin) DH_STAMP(A, 6);
@@ -329,8 +357,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
         if (threadIdx.x < nb) {
             const int i = threadIdx.x;
             double sm[4] = {0.0, 0.0, 0.0, 0.0};
-            for (int j = 0; j < 4; ++j)
-                for (int w = 0; w < kWaves; ++w) sm[j] += red[i][j][w];
+            for (int j = 0; j < 4; ++j) sm[j] += red[i][j];
             const double* c = shc[i];
             double* cs = A.consts + (b0 + i) * kConsts;
             cs[0] = sm[0];
@@ -1191,11 +1218,36 @@ struct DevBuf {
     }
 };
 
-// Threads per table.  The split path's table kernel always runs 64 (one wave per table, which
-// also defines the canonical order of the per-table k-sums); the fused kernel takes one entry per
-// thread up to N = 256 (latency) and re-forms the k-sums in the 64-lane order from LDS.
-int table_tpt(int) { return 64; }
+// Threads per table.  The fused kernel takes one entry per thread up to N = 256 (latency).  The
+// split path's table kernel takes the slot width (64, 128 or 256 threads; 64 = one wave per table
+// defines the canonical order of the k-sums, which the others re-form from LDS) that minimises
+// rounds of resident slots x entries per thread; 64 unless a wider slot saves >= 10% (requests
+// with few tables per slot, e.g. C3: 4,200 tables on 3,072 one-wave slots).
+struct dh_ctx_view {
+    int resident[3] = {0, 0, 0};
+};
+
 int fused_tpt(int N) { return N <= 64 ? 64 : (N <= 128 ? 128 : 256); }
+
+int table_tpt(const dh_ctx_view& v, int64_t n_q, int N) {
+    auto cost = [&](int i) {
+        const int tpt = 64 << i;
+        const int64_t slots = (int64_t)std::max(1, v.resident[i]) * (kBlock / tpt);
+        return (double)((n_q + slots - 1) / slots) * (double)((N + tpt - 1) / tpt);
+    };
+    const double c64 = cost(0);
+    int best = 0;
+    double bc = c64;
+    for (int i = 1; i < 3; ++i) {
+        if ((64 << i) > N) break;
+        const double c = cost(i);
+        if (c < bc && c <= 0.9 * c64) {
+            best = i;
+            bc = c;
+        }
+    }
+    return 64 << best;
+}
 
 // option-kernel threads per task: enough lanes for ceil(nopt/kR) groups, LDS permitting
 int option_tpt(int max_nopt, int N, int cap) {
@@ -1214,7 +1266,7 @@ struct dh_ctx {
     DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, cl_mask,
         cl_price, aux0, aux1, aux2, aux3;
     bool attr_set = false;
-    int table_resident = 0;   // resident cos_table_kernel<64> blocks, whole chip
+    dh_ctx_view view;          // resident cos_table_kernel<64/128/256> blocks, whole chip
     int exact = 0;          // validation mode: every option through the per-term exact path
     int path = DH_PATH_AUTO;   // fused / split request kernels (dh_ctx_set_path)
     int last_path = 0;         // kernels of the last fast-path request (dh_ctx_last_path)
@@ -1264,10 +1316,15 @@ int ensure_attrs(dh_ctx* ctx) {
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)cos_table_kernel<64>,
-                                                         kBlock, 0));
-    ctx->table_resident = std::max(1, per_cu) * std::max(1, cus);
+    const void* fns[3] = {(const void*)cos_table_kernel<64>, (const void*)cos_table_kernel<128>,
+                          (const void*)cos_table_kernel<256>};
+    for (int i = 0; i < 3; ++i) {
+        // dynamic LDS at DH_MAX_N (T2 of each wider slot) so the count never overstates
+        const size_t lds = i == 0 ? 0 : (size_t)(kBlock / (64 << i)) * DH_MAX_N * sizeof(double);
+        int per_cu = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fns[i], kBlock, lds));
+        ctx->view.resident[i] = std::max(1, per_cu) * std::max(1, cus);
+    }
     ctx->attr_set = true;
     return DH_OK;
 }
@@ -1367,7 +1424,8 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     HIP_TRY(ctx->consts.reserve((size_t)chunk * tpp * kConsts * sizeof(double)));
     HIP_TRY(ctx->cl_mask.reserve((size_t)chunk * tpp * words * 8));
     HIP_TRY(ctx->cl_price.reserve((size_t)chunk * tpp * A0.max_group * sizeof(double)));
-    const int t1 = table_tpt(N);
+    const int t1 = table_tpt(ctx->view, std::min<int64_t>(A0.P, chunk) * tpp, N);
+    const size_t lds1 = t1 == 64 ? 0 : (size_t)(kBlock / t1) * N * sizeof(double);
     const int max_nopt = A0.paired ? 1 : A0.opt_cap;
     // small tiles in a large call take the lane-per-option-group kernel (decided once per call,
     // so every chunk of it runs the same arithmetic)
@@ -1395,13 +1453,17 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         A.cl_price = (double*)ctx->cl_price.ptr;
         A.stamps = ctx->stamps_on ? (unsigned long long*)ctx->stamps.ptr : nullptr;
         const int64_t n_q = A.np * tpp;
-        const int res = ctx->table_resident;
+        const int res = ctx->view.resident[t1 == 64 ? 0 : (t1 == 128 ? 1 : 2)];
         const int64_t b1 = std::min<int64_t>((n_q + kBlock / t1 - 1) / (kBlock / t1), res);
         const int64_t n_t = A.np * tasks_per_p;
         const int64_t b2 = small ? (n_t * L + kBlock - 1) / kBlock
                                  : (n_t + kBlock / t2 - 1) / (kBlock / t2);
         if (b1 > 0x7fffffffLL || b2 > 0x7fffffffLL) return fail(DH_E_ARG, "launch too large");
-        hipLaunchKernelGGL(cos_table_kernel<64>, dim3((unsigned)b1), dim3(kBlock), 0, st, A);
+        switch (t1) {
+            case 64: hipLaunchKernelGGL(cos_table_kernel<64>, dim3((unsigned)b1), dim3(kBlock), 0, st, A); break;
+            case 128: hipLaunchKernelGGL(cos_table_kernel<128>, dim3((unsigned)b1), dim3(kBlock), lds1, st, A); break;
+            default: hipLaunchKernelGGL(cos_table_kernel<256>, dim3((unsigned)b1), dim3(kBlock), lds1, st, A); break;
+        }
         HIP_TRY(hipGetLastError());
         if (small) {
             hipLaunchKernelGGL(cos_option_small_kernel, dim3((unsigned)b2), dim3(kBlock), 0, st, A, L);
