@@ -56,6 +56,7 @@ constexpr int kR = 4;             // options carried per lane in the option kern
 constexpr int kConsts = 8;        // c0, c1, c5, w0, a, b, e^b, e^a per table
 constexpr size_t kTableBudget = size_t(256) << 20;   // table workspace per chunk (MALL-sized)
 constexpr int kLdsMax = 160 * 1024;
+constexpr int kLdsDyn = kLdsMax - 4096;   // dynamic LDS cap: the kernels keep <= 4 KB static
 
 struct PriceArgs {
     const double* prm;      // [P][16]
@@ -95,7 +96,7 @@ struct PriceArgs {
 
 // In-kernel phase stamps, compiled only into the diagnostic build (make stamps): lane 0 of each
 // block of the option kernel writes s_memtime at its phase boundaries.
-constexpr int kStamps = 8;
+constexpr int kStamps = 16;
 #ifdef DH_STAMPS
 #define DH_STAMP(A, i)                                                                     \
     do {                                                                                   \
@@ -401,7 +402,7 @@ __device__ __forceinline__ double option_sum(const Consts& C, bool is_call, doub
 __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double (&dx)[kR],
                                              const double (&cg)[kR], const double (&sg)[kR],
                                              const double* tu, const double2* t26,
-                                             double (&sum)[kR]) {
+                                             const double2* sct, double (&sum)[kR]) {
 #pragma unroll
     for (int j = 0; j < kR; ++j) sum[j] = 0.0;
     double c2[kR];
@@ -415,7 +416,7 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
         const double uk = tu[k0];
 #pragma unroll
         for (int j = 0; j < kR; ++j) {
-            dh::dsincos(uk * dx[j], &sx[j], &cx[j]);
+            dh::dsincos_t(uk * dx[j], sct, &sx[j], &cx[j]);
             cp[j] = cx[j] * cg[j] + sx[j] * sg[j];              // cos((k - G) th)
             sp[j] = sx[j] * cg[j] - cx[j] * sg[j];              // sin((k - G) th)
         }
@@ -486,6 +487,7 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
         old = __hip_atomic_fetch_add(&A.counter[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     old = __shfl(old, 0, 64);
+    DH_STAMP(A, 12);
     if (old != (unsigned)A.n_tiles - 1u) return;
     double acc = 0.0, bad = 0.0;
     for (int j = t; j < A.n_tiles; j += 64) {
@@ -543,9 +545,13 @@ __device__ __forceinline__ TileLds tile_lds(double* base, int N, int cap) {
 }
 
 // lanes per group of kR options for a tile of nopt options priced by tpt threads
+// A block-wide tile (tpt == kBlock) takes any G (its partials are reduced through LDS, e.g. G = 10
+// for 100-option tiles: 250 of 256 lanes busy instead of 200 with G = 8); narrower tiles keep a
+// power of two <= 64 for the in-wave butterfly.
 __device__ __forceinline__ int group_lanes(int nopt, int N, int tpt) {
     const int R = min(kR, max(nopt, 1));
     const int ngroups = (nopt + R - 1) / R;
+    if (tpt == kBlock) return max(1, min(tpt / ngroups, N - 1));
     int G = 1;
     while (G * 2 <= tpt / max(ngroups, 1) && G < 64) G *= 2;
     while (G > 1 && G / 2 >= N - 1) G /= 2;                 // no more lanes than terms k >= 1
@@ -554,17 +560,22 @@ __device__ __forceinline__ int group_lanes(int nopt, int N, int tpt) {
 
 // Angle sums, finalisation and price / loss-term recording of one staged tile (thread t of the
 // tile's tpt).  Shared by cos_option_kernel and cos_fused_kernel, so both give the same bits.
+// A block-wide tile (tpt == kBlock; every thread of the block must call this) whose G is not a
+// power of two <= 64 reduces each group's G lane partials through LDS (red: kR x kBlock doubles)
+// in lane order; otherwise xor butterflies inside the wave.
 __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const Consts& C,
                                           double S0, double disc, int nopt, int G, int tpt, int t,
-                                          bool active, const TileLds& L) {
+                                          bool active, const TileLds& L, double* red,
+                                          const double2* sct) {
     const int N = A.N;
     const int R = min(kR, max(nopt, 1));
     const int ngroups = (nopt + R - 1) / R;
-    const int groups_per_pass = tpt / G;
+    const int groups_per_pass = max(1, tpt / G);
+    const bool lds_red = tpt == kBlock && (G > 64 || (G & (G - 1)) != 0);   // else butterflies
     for (int pass = 0; pass < ngroups; pass += groups_per_pass) {
         const int gi = pass + t / G;
         const int gl = t % G;
-        const bool gvalid = active && gi < ngroups;
+        const bool gvalid = active && t < groups_per_pass * G && gi < ngroups;
         double dx[kR], cs[kR], ss[kR];
         bool use[kR];
 #pragma unroll
@@ -578,11 +589,37 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
             ss[j] = use[j] ? sj : 0.0;
         }
         double sm[kR];
-        angle_sums_r(1 + gl, G, N, dx, cs, ss, L.tu, L.t26, sm);
+        if (pass == 0) DH_STAMP(A, 9);
+        angle_sums_r(1 + gl, G, N, dx, cs, ss, L.tu, L.t26, sct, sm);
+        if (pass == 0) DH_STAMP(A, 10);
+        if (lds_red) {
+            if (gvalid) {
+#pragma unroll
+                for (int j = 0; j < kR; ++j) red[j * kBlock + t] = sm[j];
+            }
+            __syncthreads();
+            if (pass == 0) DH_STAMP(A, 11);
+            // lane gl of group gi finalises options j = gl, gl + G, ... (< R) of the group
+            if (gvalid) {
+                for (int j = gl; j < R; j += G) {
+                    const int oi = gi * R + j;
+                    if (oi >= nopt || isnan(L.ss[oi])) continue;
+                    const double* rj = red + j * kBlock + (t - gl);
+                    double sum = 0.0;
+                    for (int l = 0; l < G; ++l) sum += rj[l];
+                    const double v = option_sum(C, L.call[oi] != 0, S0, L.K[oi], L.xK[oi],
+                                                L.exK[oi], sum);
+                    record_price(A, p, L.perm[oi], L.mkt[oi], oi, disc * v, L.sse, L.bad);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         for (int off = 1; off < G; off <<= 1) {
 #pragma unroll
             for (int j = 0; j < kR; ++j) sm[j] += __shfl_xor(sm[j], off, 64);
         }
+        if (pass == 0) DH_STAMP(A, 11);
         // every lane of the group holds the (bitwise identical) sums: lane j finalises option j
         if (G >= R) {
             double m = sm[0];
@@ -611,6 +648,9 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
     }
 }
 
+// LDS doubles of the lane partials of a block-wide tile (tile_sums' red)
+constexpr int kRedDoubles = kR * kBlock;
+
 // ----------------------------------------------------------------------------------------------
 // option kernel
 // ----------------------------------------------------------------------------------------------
@@ -632,6 +672,9 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
 
     const int cap = A.opt_cap;
     const TileLds L = tile_lds(smem + (size_t)slot * option_lds_doubles(N, cap), N, cap);
+    double* red = smem + (size_t)kTasks * option_lds_doubles(N, cap);   // TPT == kBlock only
+    __shared__ double2 sct[128];
+    dh::load_sincos_table(sct);                                // synchronised by the staging barrier
     double2* t26 = L.t26;
     double* tu = L.tu;
     double* lK = L.K;
@@ -709,7 +752,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     __syncthreads();
     DH_STAMP(A, 1);
 
-    tile_sums(A, p, C, P.S0, disc, nopt, G, TPT, t, active, L);
+    tile_sums(A, p, C, P.S0, disc, nopt, G, TPT, t, active, L, red, sct);
     DH_STAMP(A, 2);
 
     // ---- loss: fixed-order per-task partial, last arriver finalises the param set ----
@@ -952,6 +995,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
 
     // ---- prologue (thread 0) || per-option staging (wave 0 takes the last indices) ----
     if (t == 0) table_prologue(A, q, shc);
+    DH_STAMP(A, 8);
     dh::load_sincos_table(sct);
     for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
         const int m = g0 + i;
@@ -1060,7 +1104,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
     DH_STAMP(A, 3);
 
     const Consts C{0.0 + red[0][0], 0.0 + red[1][0], 0.0 + red[2][0], 0.0 + red[3][0], a, b, eb, ea};
-    if (t < tpt2) tile_sums(A, p, C, S0, disc, gn, G, tpt2, t, true, L);
+    if (t < tpt2) tile_sums(A, p, C, S0, disc, gn, G, tpt2, t, true, L, lclp + cap, sct);
     DH_STAMP(A, 4);
     if (A.part_sse) {
         __syncthreads();
@@ -1253,7 +1297,8 @@ int table_tpt(const dh_ctx_view& v, int64_t n_q, int N) {
 int option_tpt(int max_nopt, int N, int cap) {
     int tpt = max_nopt <= kR ? 64 : (max_nopt <= 4 * kR ? 128 : 256);
     while (tpt < kBlock &&
-           (size_t)(kBlock / tpt) * option_lds_doubles(N, cap) * sizeof(double) > (size_t)kLdsMax)
+           ((size_t)(kBlock / tpt) * option_lds_doubles(N, cap) + (tpt == kBlock ? kRedDoubles : 0)) *
+                   sizeof(double) > (size_t)kLdsDyn)
         tpt *= 2;
     return tpt;
 }
@@ -1305,14 +1350,14 @@ int set_device(dh_ctx* ctx) {
 int ensure_attrs(dh_ctx* ctx) {
     if (ctx->attr_set) return DH_OK;
     HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<64>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<128>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<256>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     for (const void* f : {(const void*)cos_fused_kernel<64>, (const void*)cos_fused_kernel<128>,
                           (const void*)cos_fused_kernel<256>})
-        HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax - 4096));
+        HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -1360,7 +1405,7 @@ int launch_exact(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
 constexpr int64_t kFusedMaxTables = 1024;   // auto path: fused up to this many (p, g) tables
 
 size_t fused_lds_bytes(int N, int cap) {
-    return ((size_t)option_lds_doubles(N, cap) + (size_t)cap) * sizeof(double);
+    return ((size_t)option_lds_doubles(N, cap) + (size_t)cap + kRedDoubles) * sizeof(double);
 }
 
 // One fused launch for the whole request (every group is one tile).
@@ -1406,7 +1451,7 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         const int max_nopt = A0.paired ? 1 : A0.opt_cap;
         const bool small_call = max_nopt <= kSmallTile && A0.P * tasks_per_p >= kSmallMinTasks;
         const bool fusable = (A0.paired || A0.max_group <= kTileMax) &&
-                             fused_lds_bytes(N, A0.opt_cap) <= (size_t)kLdsMax - 4096;
+                             fused_lds_bytes(N, A0.opt_cap) <= (size_t)kLdsDyn;
         // auto: fused while the request is latency-bound (few tables); large requests keep the
         // two launches, whose table kernel runs at its own occupancy
         const bool few = A0.P * (A0.paired ? 1 : A0.n_groups) <= kFusedMaxTables;
@@ -1424,7 +1469,14 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     HIP_TRY(ctx->consts.reserve((size_t)chunk * tpp * kConsts * sizeof(double)));
     HIP_TRY(ctx->cl_mask.reserve((size_t)chunk * tpp * words * 8));
     HIP_TRY(ctx->cl_price.reserve((size_t)chunk * tpp * A0.max_group * sizeof(double)));
-    const int t1 = table_tpt(ctx->view, std::min<int64_t>(A0.P, chunk) * tpp, N);
+    // Few tables per resident slot (< 2, e.g. C3's 4,200 tables on 3,072 one-wave slots): one
+    // block per kTabs tables, not persistent, so the dispatcher backfills CUs as blocks finish
+    // instead of fixing each block's share up front (a 5-vs-6-table tail cost C3 ~30% of the
+    // table kernel).  Otherwise a resident grid of persistent blocks and the slot width of
+    // table_tpt.
+    const int64_t nq_max = std::min<int64_t>(A0.P, chunk) * tpp;
+    const bool backfill = nq_max < 2 * (int64_t)ctx->view.resident[0] * (kBlock / 64);
+    const int t1 = backfill ? 64 : table_tpt(ctx->view, nq_max, N);
     const size_t lds1 = t1 == 64 ? 0 : (size_t)(kBlock / t1) * N * sizeof(double);
     const int max_nopt = A0.paired ? 1 : A0.opt_cap;
     // small tiles in a large call take the lane-per-option-group kernel (decided once per call,
@@ -1434,8 +1486,9 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     while (L * kRs < max_nopt) L *= 2;
     const int t2 = small ? kBlock : option_tpt(max_nopt, N, A0.opt_cap);
     const size_t lds2 =
-        small ? 0 : (size_t)(kBlock / t2) * option_lds_doubles(N, A0.opt_cap) * sizeof(double);
-    if (lds2 > (size_t)kLdsMax) return fail(DH_E_ARG, "COS table does not fit in LDS");
+        small ? 0 : ((size_t)(kBlock / t2) * option_lds_doubles(N, A0.opt_cap) +
+                     (t2 == kBlock ? kRedDoubles : 0)) * sizeof(double);
+    if (lds2 > (size_t)kLdsDyn) return fail(DH_E_ARG, "COS table does not fit in LDS");
     if (ctx->stamps_on) {
         const int64_t nb = std::max((chunk * tasks_per_p + kBlock / t2 - 1) / (kBlock / t2),
                                     (chunk * tpp + kBlock / t1 - 1) / (kBlock / t1));
@@ -1454,7 +1507,8 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         A.stamps = ctx->stamps_on ? (unsigned long long*)ctx->stamps.ptr : nullptr;
         const int64_t n_q = A.np * tpp;
         const int res = ctx->view.resident[t1 == 64 ? 0 : (t1 == 128 ? 1 : 2)];
-        const int64_t b1 = std::min<int64_t>((n_q + kBlock / t1 - 1) / (kBlock / t1), res);
+        const int64_t b1 = backfill ? (n_q + kBlock / t1 - 1) / (kBlock / t1)
+                                    : std::min<int64_t>((n_q + kBlock / t1 - 1) / (kBlock / t1), res);
         const int64_t n_t = A.np * tasks_per_p;
         const int64_t b2 = small ? (n_t * L + kBlock - 1) / kBlock
                                  : (n_t + kBlock / t2 - 1) / (kBlock / t2);

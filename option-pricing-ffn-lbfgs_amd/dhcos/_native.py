@@ -164,7 +164,7 @@ class Context:
         if n.value:
             _check(load().dh_ctx_read_stamps(self._h, out.ctypes.data_as(C.POINTER(C.c_ulonglong)),
                                              n.value, C.byref(n)))
-        return out.reshape(-1, 8)
+        return out.reshape(-1, 16)
 
     def synchronize(self):
         _check(load().dh_ctx_synchronize(self._h))

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--mode", default="loss")
     ap.add_argument("--path", type=int, default=0, help="0 auto, 1 split, 2 fused")
+    ap.add_argument("--dump", default="", help="save the raw [blocks, 8] stamps (.npy)")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     opts, S0, r = bench.make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
@@ -44,6 +45,8 @@ def main():
         surf.price(host[1], cfg["N"])
     st = surf.ctx.read_stamps().astype(np.int64)
     surf.ctx.debug_stamps(False)
+    if args.dump:
+        np.save(args.dump, st)
     if surf.ctx.last_path == 2:          # cos_fused_kernel: stamps 0..5 of every block
         st = st[st[:, 0] > 0]
         print(f"{args.config} {args.mode}: fused-kernel blocks {len(st)}")
@@ -54,6 +57,12 @@ def main():
                   f"max {c.max():8.0f} cycles")
         life = st[:, 5] - st[:, 0]
         print(f"  lifetime median {np.median(life):8.0f}  max {life.max():8.0f}")
+        detail = [("prologue (thread 0)", 0, 8), ("staging wait", 8, 1), ("sums: setup", 3, 9),
+                  ("sums: angle loop", 9, 10), ("sums: butterfly", 10, 11),
+                  ("sums: finalise", 11, 4), ("loss: to atomic", 4, 12), ("loss: last", 12, 5)]
+        for nm, i0, i1 in detail:
+            c = st[:, i1] - st[:, i0]
+            print(f"    {nm:20s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}")
         return
     tb = st[st[:, 4] > 0]
     print(f"{args.config} {args.mode}: table-kernel blocks {len(tb)}")
