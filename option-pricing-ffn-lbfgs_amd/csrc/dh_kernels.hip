@@ -1262,6 +1262,36 @@ struct DevBuf {
     }
 };
 
+// Pinned, device-mapped host memory (grow-only): small request inputs and outputs the kernels
+// read and write directly over PCIe, so a host-API request is one launch and one sync.
+struct HostBuf {
+    void* ptr = nullptr;       // host address
+    void* dptr = nullptr;      // device address of the same bytes
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        release();
+        const size_t want = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipHostMalloc(&ptr, want, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) {
+            ptr = nullptr;
+            return e;
+        }
+        e = hipHostGetDevicePointer(&dptr, ptr, 0);
+        if (e != hipSuccess) {
+            release();
+            return e;
+        }
+        cap = want;
+        return hipSuccess;
+    }
+    void release() {
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = dptr = nullptr;
+        cap = 0;
+    }
+};
+
 // Threads per table.  The fused kernel takes one entry per thread up to N = 256 (latency).  The
 // split path's table kernel takes the slot width (64, 128 or 256 threads; 64 = one wave per table
 // defines the canonical order of the k-sums, which the others re-form from LDS) that minimises
@@ -1310,6 +1340,7 @@ struct dh_ctx {
     hipStream_t stream = nullptr;
     DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, cl_mask,
         cl_price, aux0, aux1, aux2, aux3;
+    HostBuf h_params, h_loss;  // zero-copy inputs / outputs of small host-API loss requests
     bool attr_set = false;
     dh_ctx_view view;          // resident cos_table_kernel<64/128/256> blocks, whole chip
     int exact = 0;          // validation mode: every option through the per-term exact path
@@ -1341,6 +1372,17 @@ struct dh_surface {
 };
 
 namespace {
+
+// Busy-wait for a short request (a calibration iteration waits on it): polling hipStreamQuery
+// returns as soon as the stream drains, where hipStreamSynchronize may yield the thread.
+int spin_sync(hipStream_t st) {
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) return DH_OK;
+        if (e != hipErrorNotReady)
+            return fail(DH_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+    }
+}
 
 int set_device(dh_ctx* ctx) {
     HIP_TRY(hipSetDevice(ctx->device));
@@ -1403,6 +1445,8 @@ int launch_exact(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
 }
 
 constexpr int64_t kFusedMaxTables = 1024;   // auto path: fused up to this many (p, g) tables
+constexpr int kZeroCopyMaxSets = 1024;       // host-API loss requests up to this many param sets
+                                             // read / write through mapped host memory
 
 size_t fused_lds_bytes(int N, int cap) {
     return ((size_t)option_lds_doubles(N, cap) + (size_t)cap + kRedDoubles) * sizeof(double);
@@ -1586,6 +1630,8 @@ int dh_ctx_destroy(dh_ctx* ctx) {
                       &ctx->consts, &ctx->cl_mask, &ctx->cl_price, &ctx->aux0,
                       &ctx->aux1, &ctx->aux2, &ctx->aux3})
         b->release();
+    ctx->h_params.release();
+    ctx->h_loss.release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return DH_OK;
@@ -1857,15 +1903,35 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
     rc = set_device(ctx);
     if (rc) return rc;
     const size_t pb = (size_t)S * DH_PARAM_STRIDE * 8;
-    HIP_TRY(ctx->params.reserve(pb));
-    HIP_TRY(ctx->sse.reserve((size_t)S * 8));
-    HIP_TRY(ctx->bad.reserve((size_t)S * 4));
     double* d_prices = nullptr;
     const size_t ob = (size_t)S * s->M * 8;
     if (prices) {
         HIP_TRY(ctx->out.reserve(ob));
         d_prices = (double*)ctx->out.ptr;
     }
+    if (S <= kZeroCopyMaxSets) {
+        // calibration-sized request: the kernels read the params and write sse / n_bad through
+        // pinned, mapped host memory -- one launch and one sync, no staging copies
+        HIP_TRY(ctx->h_params.reserve(pb));
+        HIP_TRY(ctx->h_loss.reserve((size_t)S * 12));
+        std::memcpy(ctx->h_params.ptr, params, pb);
+        double* h_sse = (double*)ctx->h_loss.ptr;
+        int32_t* h_bad = (int32_t*)(h_sse + S);
+        rc = dh_surface_loss_dev(ctx, s, (const double*)ctx->h_params.dptr, S, N, L,
+                                 (double*)ctx->h_loss.dptr, (int32_t*)((double*)ctx->h_loss.dptr + S),
+                                 d_prices, ctx->stream);
+        if (rc) return rc;
+        if (prices && s->M > 0)
+            HIP_TRY(hipMemcpyAsync(prices, d_prices, ob, hipMemcpyDeviceToHost, ctx->stream));
+        rc = spin_sync(ctx->stream);
+        if (rc) return rc;
+        std::memcpy(sse, h_sse, (size_t)S * 8);
+        std::memcpy(n_bad, h_bad, (size_t)S * 4);
+        return DH_OK;
+    }
+    HIP_TRY(ctx->params.reserve(pb));
+    HIP_TRY(ctx->sse.reserve((size_t)S * 8));
+    HIP_TRY(ctx->bad.reserve((size_t)S * 4));
     HIP_TRY(hipMemcpyAsync(ctx->params.ptr, params, pb, hipMemcpyHostToDevice, ctx->stream));
     rc = dh_surface_loss_dev(ctx, s, (const double*)ctx->params.ptr, S, N, L,
                              (double*)ctx->sse.ptr, (int32_t*)ctx->bad.ptr, d_prices, ctx->stream);

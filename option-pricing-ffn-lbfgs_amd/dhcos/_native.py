@@ -50,7 +50,9 @@ SIGNATURES = {
     "dh_surface_destroy": (C.c_int, [_vp]),
     "dh_surface_size": (C.c_int, [_vp, _i32p, _i32p]),
     "dh_surface_price": (C.c_int, [_vp, _vp, _dp, C.c_int64, C.c_int, C.c_double, _dp]),
-    "dh_surface_loss": (C.c_int, [_vp, _vp, _dp, C.c_int, C.c_int, C.c_double, _dp, _i32p, _dp]),
+    # the per-iteration calibration call takes raw addresses (ndarray.ctypes.data): half the
+    # marshalling cost of data_as() pointers
+    "dh_surface_loss": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp]),
     "dh_surface_price_dev": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp, _vp]),
     "dh_surface_loss_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp,
                                       _vp]),
@@ -272,9 +274,9 @@ class Surface:
         bad = np.empty(S, dtype=np.int32)
         prices = np.empty((S, self.M)) if want_prices else None
         with self.ctx._lock:
-            _check(load().dh_surface_loss(self.ctx.handle, self._h, _ptr(params), S, int(N),
-                                          float(L), _ptr(sse), _ptr(bad, _i32p),
-                                          None if prices is None else _ptr(prices)))
+            _check(load().dh_surface_loss(self.ctx.handle, self._h, params.ctypes.data, S, int(N),
+                                          float(L), sse.ctypes.data, bad.ctypes.data,
+                                          None if prices is None else prices.ctypes.data))
         return sse, bad, prices
 
     # device-pointer variants (torch tensors or raw device addresses)

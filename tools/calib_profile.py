@@ -1,0 +1,51 @@
+"""Host-side profile of calibrate(300, 3) on a bench surface (cProfile, top functions by self time).
+
+Usage: python tools/calib_profile.py [--config c2]
+"""
+import argparse
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "option-pricing-ffn-lbfgs_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+import bench  # noqa: E402
+from dhcos.calibrator import DoubleHestonJumpCalibrator  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    args = ap.parse_args()
+    cfg = bench.CONFIGS[args.config]
+    opts, S0, r = bench.make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
+    for _ in range(2):                      # warm-up (surface upload, JIT of nothing, caches)
+        np.random.seed(0)
+        DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"]).calibrate(300, 3)
+    times = []
+    for _ in range(7):
+        cal = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"])
+        np.random.seed(0)
+        t0 = time.perf_counter()
+        cal.calibrate(300, 3)
+        times.append(time.perf_counter() - t0)
+    t_plain = float(np.median(times))
+    cal = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"])
+    np.random.seed(0)
+    pr = cProfile.Profile()
+    pr.enable()
+    cal.calibrate(300, 3)
+    pr.disable()
+    print(f"calibrate(300, 3): median of 7 {t_plain * 1e3:.2f} ms (min {min(times) * 1e3:.2f}), "
+          f"{cal.lockstep_launches} launches, "
+          f"{t_plain / cal.lockstep_launches * 1e6:.1f} us per launch")
+    pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+
+
+if __name__ == "__main__":
+    main()
