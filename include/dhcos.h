@@ -117,6 +117,51 @@ int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params
                         double L, double* d_sse, int32_t* d_n_bad, double* d_prices,
                         void* stream);
 
+/* ---- device-resident multi-start L-BFGS-B ------------------------------------------------- */
+/* Runs S independent L-BFGS-B starts (no bounds) on the surface's calibration loss without a
+ * host round trip per iteration.  Replaces the per-start
+ *   minimize(compute_loss, x0, method='L-BFGS-B', options={maxiter, ftol, gtol})
+ * of DoubleHestonJumpCalibrator.calibrate (lbfgs_calibrator.py:259-269, SciPy's 2-point
+ * forward-difference gradient at h = 1e-8, scipy/optimize/_numdiff.py:498-511,592-596).
+ * Each iteration is one loss launch over the 14 x (live starts) points of every live start's
+ * pending function+gradient request, then one step launch (one wave per start) that forms
+ * loss = n_bad ? 1e10 : sse / M + Feller penalty and the FD gradient, advances the start's
+ * L-BFGS-B state (csrc/dh_lbfgs.h) to its next request and writes that request's 14 param
+ * records.  The host only checks for finished starts every `chunk` iterations.
+ * x0: [S][13] unconstrained start points (lbfgs_calibrator.py:62-87 transform), S0 / r the
+ * spot and rate of every record.  Results per start in out[S].                                */
+typedef struct {
+    int32_t maxiter;             /* NEW_X iterations (minimize's maxiter) */
+    int32_t maxfun;              /* stop when requests (x0 included) > maxfun at a NEW_X */
+    int32_t maxls;               /* line-search trial points (SciPy default 20) */
+    int32_t chunk;               /* iterations enqueued between host checks (<= 0: 8) */
+    double ftol;                 /* relative-reduction test: factr = ftol / eps */
+    double gtol;                 /* projected-gradient test */
+} dh_lb_options;
+
+typedef struct {
+    double x[13];                /* final x (restored start of the last line search if ABNORMAL) */
+    double fun;                  /* f of the LAST evaluated point, as SciPy's OptimizeResult.fun */
+    double best_loss;            /* smallest valid loss this start evaluated (:171-172) */
+    double t_done;               /* seconds from the call until the host saw the start finish */
+    int32_t nit;                 /* NEW_X iterations */
+    int32_t nfev;                /* function+gradient requests, x0 included */
+    int32_t task;                /* SciPy status*1000 + message: 4401/4402 CONVERGENCE,
+                                    5502/5504 STOP, 8000 ABNORMAL, 7000 ERROR (line search) */
+    int32_t warnflag;            /* 0 converged, 1 maxfun/maxiter, 2 other */
+    int32_t n_calls;             /* loss evaluations (14 per request) */
+    int32_t pad;
+} dh_lb_result;
+
+int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double* x0, int S, double S0,
+                       double r, int N, double L, const dh_lb_options* opt, dh_lb_result* out,
+                       int32_t* n_launches);
+/* Diagnostics (tests): with cap > 0, dh_calibrate_lbfgs records every consumed request as 32
+ * doubles [start, request number, f, x[13], g[13], 0 0 0] (order across starts arbitrary);
+ * dh_ctx_read_lb_trace copies up to cap records of the last call and sets *n to the count.     */
+int dh_ctx_set_lb_trace(dh_ctx* ctx, int64_t cap);
+int dh_ctx_read_lb_trace(dh_ctx* ctx, double* out, int64_t cap, int64_t* n);
+
 /* ---- paired pricing: option i under param set i ------------------------------------------- */
 /* out[i] = price of (K[i], T[i], is_call[i]) under params[i]; replaces a loop of single
  * DoubleHeston(...).pricing(N) calls (double_heston.py:160-192).                              */

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <numeric>
@@ -42,6 +43,7 @@
 #include <vector>
 
 #include "dh_device.h"
+#include "dh_lbfgs.h"
 #include "dhcos.h"
 
 using dh::cplx;
@@ -92,7 +94,16 @@ struct PriceArgs {
     unsigned long long* cl_mask;   // workspace: [np*tabs_per_p][cl_words] clamp bits per option
     double* cl_price;       // workspace: [np*tabs_per_p][max_group] prices of clamped options
     unsigned long long* stamps;   // diagnostic builds (DH_STAMPS) only: [blocks][kStamps]
+    const int* live_count;  // device-resident calibration: the launch is a no-op once every start
+                            // has finished (*live_count == 0), else null
 };
+
+// A launch enqueued ahead by dh_calibrate_lbfgs after its starts have all finished returns at
+// once.  The count only changes between launches (the step kernel writes it), so every block of
+// a launch takes the same branch and the loss hand-off counters stay consistent.
+__device__ __forceinline__ bool halted(const PriceArgs& A) {
+    return A.live_count && __builtin_amdgcn_readfirstlane(*A.live_count) <= 0;
+}
 
 // In-kernel phase stamps, compiled only into the diagnostic build (make stamps): lane 0 of each
 // block of the option kernel writes s_memtime at its phase boundaries.
@@ -221,6 +232,7 @@ constexpr int kBatch = 64;
 // re-form the same sums in the same order, so every slot width gives the same bits.
 template <int TPT>
 __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(PriceArgs A) {
+    if (halted(A)) return;
     constexpr int kTabs = kBlock / TPT;      // table slots per block
     extern __shared__ __attribute__((aligned(16))) double t2s[];   // TPT > 64: [kTabs][N] T2_k
     __shared__ double shc[kBatch][kTabC];
@@ -656,6 +668,7 @@ constexpr int kRedDoubles = kR * kBlock;
 // ----------------------------------------------------------------------------------------------
 template <int TPT>
 __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(PriceArgs A) {
+    if (halted(A)) return;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int kTasks = kBlock / TPT;
     const int slot = threadIdx.x / TPT;
@@ -780,6 +793,7 @@ constexpr int kRs = 4;
 constexpr int64_t kSmallMinTasks = 65536;
 
 __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, int L) {
+    if (halted(A)) return;
     const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t n_tasks = A.paired ? A.np : A.np * (int64_t)A.n_tiles;
     const int64_t task_l = gid / L;
@@ -963,6 +977,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
 // ----------------------------------------------------------------------------------------------
 template <int TPT1>
 __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(PriceArgs A, int tpt2) {
+    if (halted(A)) return;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ double shc[kTabC];
     __shared__ double red[4][1];
@@ -1341,6 +1356,11 @@ struct dh_ctx {
     DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, cl_mask,
         cl_price, aux0, aux1, aux2, aux3;
     HostBuf h_params, h_loss;  // zero-copy inputs / outputs of small host-API loss requests
+    DevBuf lb_state, lb_rec, lb_sse, lb_bad, lb_live, lb_done, lb_x0;   // dh_calibrate_lbfgs
+    HostBuf h_lb;              // finished flags / live list of dh_calibrate_lbfgs
+    DevBuf lb_trace, lb_trace_n;   // diagnostic request trace of dh_calibrate_lbfgs
+    hipEvent_t lb_ev[2] = {nullptr, nullptr};   // chunk-completion events of dh_calibrate_lbfgs
+    int64_t lb_trace_cap = 0;
     bool attr_set = false;
     dh_ctx_view view;          // resident cos_table_kernel<64/128/256> blocks, whole chip
     int exact = 0;          // validation mode: every option through the per-term exact path
@@ -1628,10 +1648,15 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     for (DevBuf* b : {&ctx->params, &ctx->out, &ctx->sse, &ctx->bad, &ctx->part_sse,
                       &ctx->part_bad, &ctx->counter, &ctx->exact_prices, &ctx->stamps, &ctx->table,
                       &ctx->consts, &ctx->cl_mask, &ctx->cl_price, &ctx->aux0,
-                      &ctx->aux1, &ctx->aux2, &ctx->aux3})
+                      &ctx->aux1, &ctx->aux2, &ctx->aux3, &ctx->lb_state, &ctx->lb_rec,
+                      &ctx->lb_sse, &ctx->lb_bad, &ctx->lb_live, &ctx->lb_done, &ctx->lb_x0,
+                      &ctx->lb_trace, &ctx->lb_trace_n})
         b->release();
     ctx->h_params.release();
     ctx->h_loss.release();
+    ctx->h_lb.release();
+    for (hipEvent_t e : ctx->lb_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return DH_OK;
@@ -1835,9 +1860,11 @@ int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_param
     return launch_price(ctx, A, stream ? (hipStream_t)stream : ctx->stream);
 }
 
-int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S, int N,
-                        double L, double* d_sse, int32_t* d_n_bad, double* d_prices,
-                        void* stream) {
+}  // extern "C"
+
+static int surface_loss_launch(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S,
+                               int N, double L, double* d_sse, int32_t* d_n_bad,
+                               double* d_prices, void* stream, const int* live_count) {
     if (!ctx || !s || (S > 0 && (!d_params || !d_sse || !d_n_bad)))
         return fail(DH_E_ARG, "null argument");
     if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
@@ -1869,7 +1896,17 @@ int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params
     A.counter = (unsigned*)ctx->counter.ptr;
     A.sse = d_sse;
     A.n_bad = (int*)d_n_bad;
+    A.live_count = live_count;
     return launch_price(ctx, A, st);
+}
+
+extern "C" {
+
+int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S, int N,
+                        double L, double* d_sse, int32_t* d_n_bad, double* d_prices,
+                        void* stream) {
+    return surface_loss_launch(ctx, s, d_params, S, N, L, d_sse, d_n_bad, d_prices, stream,
+                               nullptr);
 }
 
 int dh_surface_price(dh_ctx* ctx, const dh_surface* s, const double* params, int64_t P, int N,
@@ -2070,3 +2107,459 @@ int dh_cos_coeffs(dh_ctx* ctx, const int32_t* k, int n, double c, double d, doub
 }
 
 }  // extern "C"
+
+// ----------------------------------------------------------------------------------------------
+// device-resident multi-start L-BFGS-B (dh_calibrate_lbfgs)
+// ----------------------------------------------------------------------------------------------
+// Nothing below is contracted into FMAs: the step kernel must compute the bits of the CPU build
+// of dh_lbfgs.h (tests/native/lb_host.cpp).
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr double kInvalidLoss = 1e10;                 // lbfgs_calibrator.py:152-158,176-177
+constexpr double kFdStep = 1e-8;                      // SciPy L-BFGS-B eps
+constexpr double kSqrtEps = 1.4901161193847656e-08;   // sqrt(DBL_EPSILON), _numdiff fallback
+
+// A 13-vector held one component per lane (lanes 13..63 hold 0).  Reductions are DPP
+// butterflies inside each 16-lane row -- quad_perm [1,0,3,2], quad_perm [2,3,0,1],
+// row_half_mirror, row_mirror -- in which both partners add the same two operands, so every lane
+// of the row ends with the same bits: the pairwise tree ((p0+p1)+(p2+p3)) + ... that
+// tests/native/lb_host.cpp reproduces.
+struct WaveVec {
+    double v;
+};
+__device__ __forceinline__ WaveVec operator+(WaveVec a, WaveVec b) { return {a.v + b.v}; }
+__device__ __forceinline__ WaveVec operator-(WaveVec a, WaveVec b) { return {a.v - b.v}; }
+__device__ __forceinline__ WaveVec operator-(WaveVec a) { return {-a.v}; }
+__device__ __forceinline__ WaveVec operator*(double s, WaveVec a) { return {s * a.v}; }
+
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, Ctrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), Ctrl, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
+__device__ __forceinline__ double row_sum(double p) {
+    p = p + dpp_f64<kDppXor1>(p);
+    p = p + dpp_f64<kDppXor2>(p);
+    p = p + dpp_f64<kDppHalfMirror>(p);
+    return p + dpp_f64<kDppMirror>(p);
+}
+__device__ __forceinline__ double row_max(double m) {
+    m = fmax(m, dpp_f64<kDppXor1>(m));
+    m = fmax(m, dpp_f64<kDppXor2>(m));
+    m = fmax(m, dpp_f64<kDppHalfMirror>(m));
+    return fmax(m, dpp_f64<kDppMirror>(m));
+}
+__device__ __forceinline__ double row_min(double m) {
+    m = fmin(m, dpp_f64<kDppXor1>(m));
+    m = fmin(m, dpp_f64<kDppXor2>(m));
+    m = fmin(m, dpp_f64<kDppHalfMirror>(m));
+    return fmin(m, dpp_f64<kDppMirror>(m));
+}
+__device__ __forceinline__ double dot(WaveVec a, WaveVec b) { return row_sum(a.v * b.v); }
+__device__ __forceinline__ double amax(WaveVec a) { return fmax(0.0, row_max(fabs(a.v))); }
+__device__ __forceinline__ bool equal(WaveVec a, WaveVec b) { return __all(a.v == b.v); }
+
+// The pair memory in LDS: s_j, y_j as 16-double rows (lane i reads column i), dr_j and the
+// two-loop's alpha_j.  Every lane computes the same scalars, so the scalar writes are uniform.
+struct WaveRing {
+    double* rs;                // [kM][16]
+    double* ry;                // [kM][16]
+    double* rdr;               // [kM]
+    double* ra;                // [kM]
+    int lane;
+    __device__ WaveVec s(int j) const { return {lane < dhlb::kLanes ? rs[j * dhlb::kLanes + lane] : 0.0}; }
+    __device__ WaveVec y(int j) const { return {lane < dhlb::kLanes ? ry[j * dhlb::kLanes + lane] : 0.0}; }
+    __device__ double dr(int j) const { return rdr[j]; }
+    __device__ double& a(int j) { return ra[j]; }
+    __device__ void put(int j, WaveVec sj, WaveVec yj, double d) {
+        if (lane < dhlb::kLanes) {
+            rs[j * dhlb::kLanes + lane] = sj.v;
+            ry[j * dhlb::kLanes + lane] = yj.v;
+        }
+        rdr[j] = d;
+    }
+    __device__ void shift() {
+        for (int j = 0; j + 1 < dhlb::kM; ++j) {
+            if (lane < dhlb::kLanes) {
+                rs[j * dhlb::kLanes + lane] = rs[(j + 1) * dhlb::kLanes + lane];
+                ry[j * dhlb::kLanes + lane] = ry[(j + 1) * dhlb::kLanes + lane];
+            }
+            rdr[j] = rdr[j + 1];
+        }
+    }
+};
+
+using WaveCore = dhlb::LbCore<WaveVec, WaveRing>;
+
+// diagnostic trace record of one consumed request: start, request number, f, x[13], g[13]
+constexpr int kLbTrace = 32;
+
+// Global state of one start: the vectors as 16-double rows (lane i holds column i), the pair
+// memory (staged in LDS by the step kernel), then the scalars.
+constexpr int kLbVecs = 10;                           // x g z d t r xe ge dx pen
+constexpr int kLbRing = 2 * dhlb::kM * dhlb::kLanes + dhlb::kM;   // s rows, y rows, dr
+struct LbSlot {
+    double vec[kLbVecs][dhlb::kLanes];
+    double ring[kLbRing];
+    dhlb::LbScalars s;
+};
+
+struct LbArgs {
+    LbSlot* states;            // [S]
+    const int* live;           // [n_live] start index of each slot
+    const double* x0;          // [S][13] (mode 0)
+    const double* sse;         // [n_live * 14] loss partial sums of the last request, slot-major
+    const int* bad;            // [n_live * 14]
+    double* rec;               // [n_live * 14][16] param records of the next request
+    int* done;                 // [S] finished flags (pinned host memory, read between chunks)
+    int* live_count;           // starts not finished yet (the loss launches halt at 0)
+    double* trace;             // diagnostic: [trace_cap][kLbTrace] consumed requests, or null
+    unsigned long long* trace_n;
+    int64_t trace_cap;
+    dhlb::LbConfig cfg;
+    double S0, r;
+    int M;
+    int mode;                  // 0 begin at x0, 1 consume the request and advance, 2 re-emit
+};
+
+__device__ __forceinline__ WaveVec lb_ld(const LbSlot* g, int v, int lane) {
+    return {lane < dhlb::kLanes ? g->vec[v][lane] : 0.0};
+}
+
+__device__ __forceinline__ void lb_st(LbSlot* g, int v, int lane, WaveVec x) {
+    if (lane < dhlb::kLanes) g->vec[v][lane] = x.v;
+}
+
+// model parameter i from unconstrained x_i (lbfgs_calibrator.py:62-87): tanh for the two
+// correlations, identity for mu_j, exp otherwise
+__device__ __forceinline__ double lb_transform(int i, double x) {
+    if (i == 4 || i == 9) return tanh(x);
+    if (i == 11) return x;
+    return exp(x);
+}
+
+// Emit the pending request at xe.  Lane i < 13 maps x_i and x_i + h_i (SciPy's step rule,
+// scipy/optimize/_numdiff.py:498-511) to model params and keeps dx_i = (x_i + h_i) - x_i; lane
+// t < 14 assembles point t (x, or x + h_{t-1} e_{t-1}), writes its record and keeps its Feller
+// penalty (lbfgs_calibrator.py:113-116) in pen.
+__device__ void lb_emit(const WaveCore& c, WaveVec& dx, WaveVec& pen, double* pb, double* pp,
+                        const LbArgs& A, int slot, int lane) {
+    if (lane < dhlb::kN) {
+        const double xi = c.xe.v;
+        double h = kFdStep;
+        if ((xi + h) - xi == 0.0) h = kSqrtEps * (xi >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(xi));
+        const double xh = xi + h;
+        dx.v = xh - xi;
+        pb[lane] = lb_transform(lane, xi);
+        pp[lane] = lb_transform(lane, xh);
+    } else {
+        dx.v = 0.0;
+    }
+    __syncthreads();
+    pen.v = 0.0;
+    if (lane < dhlb::kPts) {
+        double p[dhlb::kN];
+#pragma unroll
+        for (int i = 0; i < dhlb::kN; ++i) p[i] = (i == lane - 1) ? pp[i] : pb[i];
+        const double v1 = p[3] * p[3] - 2.0 * p[1] * p[2];
+        const double v2 = p[8] * p[8] - 2.0 * p[6] * p[7];
+        pen.v = 1000.0 * ((v1 > 0.0 ? v1 : 0.0) + (v2 > 0.0 ? v2 : 0.0));
+        double* out = A.rec + ((size_t)slot * dhlb::kPts + lane) * DH_PARAM_STRIDE;
+#pragma unroll
+        for (int i = 0; i < dhlb::kN; ++i) out[i] = p[i];
+        out[13] = A.S0;
+        out[14] = A.r;
+        out[15] = 0.0;
+    }
+}
+
+// One wave per live start: load the state (vectors into registers, lane i = component i; the
+// pair memory into LDS), consume the finished request (lane t forms loss t, lane i gradient
+// component i), run the L-BFGS-B state machine until it needs a new point, emit that request,
+// store the state.
+__global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
+    __shared__ double ring[kLbRing + dhlb::kM];
+    __shared__ double fl[dhlb::kLanes];
+    __shared__ double pb[dhlb::kLanes], pp[dhlb::kLanes];
+    const int slot = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int sidx = A.live[slot];
+    LbSlot* G = A.states + sidx;
+    WaveCore c;
+    c.pairs = WaveRing{ring, ring + dhlb::kM * dhlb::kLanes, ring + 2 * dhlb::kM * dhlb::kLanes,
+                       ring + kLbRing, lane};
+    WaveVec dx, pen;
+    if (A.mode == 0) {
+        c.s = dhlb::LbScalars{};
+        const WaveVec z{0.0};
+        c.x = c.g = c.z = c.d = c.t = c.r = c.ge = z;
+        for (int i = lane; i < kLbRing + dhlb::kM; i += 64) ring[i] = 0.0;
+        const WaveVec x0{lane < dhlb::kN ? A.x0[(size_t)sidx * dhlb::kN + lane] : 0.0};
+        dhlb::lb_begin(c, x0);
+        c.s.best_loss = __builtin_huge_val();
+        c.s.n_calls = 0;
+    } else {
+        c.s = G->s;
+        if (c.s.done) return;                          // uniform across the wave
+        for (int i = lane; i < kLbRing; i += 64) ring[i] = G->ring[i];
+        c.x = lb_ld(G, 0, lane);
+        c.g = lb_ld(G, 1, lane);
+        c.z = lb_ld(G, 2, lane);
+        c.d = lb_ld(G, 3, lane);
+        c.t = lb_ld(G, 4, lane);
+        c.r = lb_ld(G, 5, lane);
+        c.xe = lb_ld(G, 6, lane);
+        c.ge = lb_ld(G, 7, lane);
+        dx = lb_ld(G, 8, lane);
+        pen = lb_ld(G, 9, lane);
+    }
+    int need = 1;
+    if (A.mode == 1) {
+        double f = __builtin_huge_val();
+        if (lane < dhlb::kPts) {
+            const size_t i = (size_t)slot * dhlb::kPts + lane;
+            f = A.bad[i] > 0 ? kInvalidLoss : A.sse[i] / (double)A.M + pen.v;
+        }
+        if (lane < dhlb::kLanes) fl[lane] = f;
+        __syncthreads();
+        const double lo = row_min((f == f && f != kInvalidLoss) ? f : __builtin_huge_val());
+        c.s.n_calls += dhlb::kPts;
+        if (lo < c.s.best_loss) c.s.best_loss = lo;
+        c.s.fe = fl[0];
+        c.ge.v = lane < dhlb::kN ? (fl[lane + 1] - fl[0]) / dx.v : 0.0;
+        if (A.trace) {
+            unsigned long long k = 0;
+            if (lane == 0) k = atomicAdd(A.trace_n, 1ull);
+            k = __shfl(k, 0, 64);
+            if ((int64_t)k < A.trace_cap) {
+                double* tr = A.trace + k * kLbTrace;
+                if (lane == 0) {
+                    tr[0] = sidx;
+                    tr[1] = c.s.n_calls / dhlb::kPts - 1;
+                    tr[2] = c.s.fe;
+                }
+                if (lane < dhlb::kN) {
+                    tr[3 + lane] = c.xe.v;
+                    tr[3 + dhlb::kN + lane] = c.ge.v;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (A.mode == 1) {
+        need = dhlb::lb_resume(c, A.cfg);
+        if (!need && lane == 0) {
+            __hip_atomic_store(&A.done[sidx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            atomicSub(A.live_count, 1);
+        }
+    }
+    if (need) lb_emit(c, dx, pen, pb, pp, A, slot, lane);
+    __syncthreads();
+    for (int i = lane; i < kLbRing; i += 64) G->ring[i] = ring[i];
+    lb_st(G, 0, lane, c.x);
+    lb_st(G, 1, lane, c.g);
+    lb_st(G, 2, lane, c.z);
+    lb_st(G, 3, lane, c.d);
+    lb_st(G, 4, lane, c.t);
+    lb_st(G, 5, lane, c.r);
+    lb_st(G, 6, lane, c.xe);
+    lb_st(G, 7, lane, c.ge);
+    lb_st(G, 8, lane, dx);
+    lb_st(G, 9, lane, pen);
+    if (lane == 0) G->s = c.s;
+}
+
+int launch_lb_step(hipStream_t st, const LbArgs& A, int n_live) {
+    hipLaunchKernelGGL(lb_step_kernel, dim3((unsigned)n_live), dim3(64), 0, st, A);
+    HIP_TRY(hipGetLastError());
+    return DH_OK;
+}
+
+}  // namespace
+
+extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double* x0, int S,
+                                  double S0, double r, int N, double L, const dh_lb_options* opt,
+                                  dh_lb_result* out, int32_t* n_launches) {
+    if (!ctx || !s || !opt || (S > 0 && (!x0 || !out))) return fail(DH_E_ARG, "null argument");
+    if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
+    if (s->M == 0) return fail(DH_E_ARG, "empty market (the loss is NaN; no optimisation)");
+    int rc = check_N(N);
+    if (rc) return rc;
+    if (S < 0) return fail(DH_E_ARG, "S < 0");
+    if (opt->maxiter < 1 || opt->maxfun < 1 || opt->maxls < 1)
+        return fail(DH_E_ARG, "maxiter, maxfun and maxls must be >= 1");
+    if (n_launches) *n_launches = 0;
+    if (S == 0) return DH_OK;
+    rc = set_device(ctx);
+    if (rc) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    hipStream_t st = ctx->stream;
+    const size_t npts = (size_t)S * dhlb::kPts;
+    HIP_TRY(ctx->lb_state.reserve((size_t)S * sizeof(LbSlot)));
+    HIP_TRY(ctx->lb_rec.reserve(npts * DH_PARAM_STRIDE * 8));
+    HIP_TRY(ctx->lb_sse.reserve(npts * 8));
+    HIP_TRY(ctx->lb_bad.reserve(npts * 4));
+    HIP_TRY(ctx->lb_live.reserve((size_t)S * 4));
+    HIP_TRY(ctx->lb_done.reserve(4));                  // live-start count (halts launches at 0)
+    HIP_TRY(ctx->lb_x0.reserve((size_t)S * dhlb::kN * 8));
+    // pinned, device-mapped: finished flags (written by the step kernel) | 2 live-list buffers
+    HIP_TRY(ctx->h_lb.reserve((size_t)S * 3 * 4));
+    int* h_done = (int*)ctx->h_lb.ptr;
+    int* h_live[2] = {h_done + S, h_done + 2 * S};
+    std::memset(h_done, 0, (size_t)S * 4);
+    std::vector<int> live(S);
+    for (int i = 0; i < S; ++i) live[i] = h_live[0][i] = i;
+    HIP_TRY(hipMemcpyAsync(ctx->lb_x0.ptr, x0, (size_t)S * dhlb::kN * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->lb_live.ptr, h_live[0], (size_t)S * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)ctx->lb_done.ptr, S, 1, st));
+    if (!ctx->lb_ev[0]) {
+        for (hipEvent_t& e : ctx->lb_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+
+    LbArgs A;
+    A.states = (LbSlot*)ctx->lb_state.ptr;
+    A.live = (const int*)ctx->lb_live.ptr;
+    A.x0 = (const double*)ctx->lb_x0.ptr;
+    A.sse = (const double*)ctx->lb_sse.ptr;
+    A.bad = (const int*)ctx->lb_bad.ptr;
+    A.rec = (double*)ctx->lb_rec.ptr;
+    A.done = (int*)ctx->h_lb.dptr;
+    A.live_count = (int*)ctx->lb_done.ptr;
+    A.trace = nullptr;
+    A.trace_n = nullptr;
+    A.trace_cap = 0;
+    if (ctx->lb_trace_cap > 0) {
+        HIP_TRY(ctx->lb_trace.reserve((size_t)ctx->lb_trace_cap * kLbTrace * 8));
+        HIP_TRY(ctx->lb_trace_n.reserve(8));
+        HIP_TRY(hipMemsetAsync(ctx->lb_trace_n.ptr, 0, 8, st));
+        A.trace = (double*)ctx->lb_trace.ptr;
+        A.trace_n = (unsigned long long*)ctx->lb_trace_n.ptr;
+        A.trace_cap = ctx->lb_trace_cap;
+    }
+    A.cfg.maxiter = opt->maxiter;
+    A.cfg.maxfun = opt->maxfun;
+    A.cfg.maxls = opt->maxls;
+    A.cfg.pad = 0;
+    A.cfg.factr_epsmch = (opt->ftol / dhlb::kEpsMch) * dhlb::kEpsMch;   // factr * epsmch
+    A.cfg.pgtol = opt->gtol;
+    A.S0 = S0;
+    A.r = r;
+    A.M = s->M;
+    A.mode = 0;
+    rc = launch_lb_step(st, A, S);
+    if (rc) return rc;
+
+    // Chunks of `chunk` iterations (loss launch(es) + step launch) are enqueued two ahead of the
+    // host: while the GPU runs chunk k + 1, the host reads the finished flags as of the end of
+    // chunk k, compacts the live starts (their requests are re-emitted at the new slots, in
+    // stream order after chunk k + 1) and enqueues chunk k + 2.  Launches enqueued after the
+    // last start finished return at once (live count 0).
+    const int chunk = opt->chunk > 0 ? opt->chunk : 8;
+    const int64_t max_iters = (int64_t)opt->maxfun + 2LL * opt->maxls + 8;   // nfev bound per start
+    std::vector<double> t_done(S, 0.0);
+    int n_live = S;
+    int64_t iters = 0, launches = 0;
+    auto enqueue_chunk = [&](int k) -> int {
+        A.mode = 1;
+        for (int c = 0; c < chunk; ++c) {
+            int e = surface_loss_launch(ctx, s, A.rec, n_live * dhlb::kPts, N, L, (double*)A.sse,
+                                        (int32_t*)A.bad, nullptr, st, A.live_count);
+            if (e) return e;
+            e = launch_lb_step(st, A, n_live);
+            if (e) return e;
+            ++launches;
+        }
+        iters += chunk;
+        HIP_TRY(hipEventRecord(ctx->lb_ev[k & 1], st));
+        return DH_OK;
+    };
+    rc = enqueue_chunk(0);
+    if (rc) return rc;
+    rc = enqueue_chunk(1);
+    if (rc) return rc;
+    for (int k = 0;; ++k) {
+        for (;;) {                                     // spin: a chunk is ~0.1-1 ms
+            const hipError_t e = hipEventQuery(ctx->lb_ev[k & 1]);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady)
+                return fail(DH_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
+        }
+        const double now =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::vector<int> next;
+        next.reserve(live.size());
+        for (int sidx : live) {
+            if (__atomic_load_n(&h_done[sidx], __ATOMIC_ACQUIRE)) {
+                if (t_done[sidx] == 0.0) t_done[sidx] = now;
+            } else {
+                next.push_back(sidx);
+            }
+        }
+        if (next.empty()) break;
+        if (iters > max_iters) {
+            (void)hipStreamSynchronize(st);
+            return fail(DH_E_ARG, "L-BFGS-B starts did not terminate");
+        }
+        if (next.size() != live.size()) {              // compact; re-emit their requests
+            live.swap(next);
+            n_live = (int)live.size();
+            int* hl = h_live[(k + 1) & 1];             // the other buffer's upload has run
+            std::memcpy(hl, live.data(), (size_t)n_live * 4);
+            HIP_TRY(hipMemcpyAsync(ctx->lb_live.ptr, hl, (size_t)n_live * 4,
+                                   hipMemcpyHostToDevice, st));
+            A.mode = 2;
+            rc = launch_lb_step(st, A, n_live);
+            if (rc) return rc;
+        }
+        rc = enqueue_chunk(k + 2);
+        if (rc) return rc;
+    }
+    std::vector<LbSlot> hs(S);
+    HIP_TRY(hipMemcpyAsync(hs.data(), ctx->lb_state.ptr, (size_t)S * sizeof(LbSlot),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int i = 0; i < S; ++i) {
+        const LbSlot& q = hs[i];
+        dh_lb_result& o = out[i];
+        for (int j = 0; j < dhlb::kN; ++j) o.x[j] = q.vec[0][j];   // row 0 = x
+        o.fun = q.s.fe;
+        o.best_loss = q.s.best_loss;
+        o.t_done = t_done[i];
+        o.nit = q.s.nit;
+        o.nfev = q.s.nfev;
+        o.task = q.s.task;
+        o.warnflag = q.s.warnflag;
+        o.n_calls = q.s.n_calls;
+        o.pad = 0;
+    }
+    if (n_launches) *n_launches = (int32_t)launches;
+    return DH_OK;
+}
+
+extern "C" int dh_ctx_set_lb_trace(dh_ctx* ctx, int64_t cap) {
+    if (!ctx) return fail(DH_E_ARG, "null argument");
+    if (cap < 0) return fail(DH_E_ARG, "cap < 0");
+    ctx->lb_trace_cap = cap;
+    return DH_OK;
+}
+
+extern "C" int dh_ctx_read_lb_trace(dh_ctx* ctx, double* out, int64_t cap, int64_t* n) {
+    if (!ctx || !n || (cap > 0 && !out)) return fail(DH_E_ARG, "null argument");
+    *n = 0;
+    if (ctx->lb_trace_cap == 0 || !ctx->lb_trace_n.ptr) return DH_OK;
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    unsigned long long cnt = 0;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(&cnt, ctx->lb_trace_n.ptr, 8, hipMemcpyDeviceToHost));
+    const int64_t m = std::min<int64_t>({(int64_t)cnt, ctx->lb_trace_cap, cap});
+    if (m > 0) HIP_TRY(hipMemcpy(out, ctx->lb_trace.ptr, (size_t)m * kLbTrace * 8, hipMemcpyDeviceToHost));
+    *n = (int64_t)cnt;
+    return DH_OK;
+}

@@ -31,6 +31,20 @@ _i8p = C.POINTER(C.c_int8)
 _i32p = C.POINTER(C.c_int32)
 _vp = C.c_void_p
 
+
+class LbOptions(C.Structure):
+    """dh_lb_options (include/dhcos.h)."""
+    _fields_ = [("maxiter", C.c_int32), ("maxfun", C.c_int32), ("maxls", C.c_int32),
+                ("chunk", C.c_int32), ("ftol", C.c_double), ("gtol", C.c_double)]
+
+
+class LbResult(C.Structure):
+    """dh_lb_result (include/dhcos.h): one finished L-BFGS-B start."""
+    _fields_ = [("x", C.c_double * 13), ("fun", C.c_double), ("best_loss", C.c_double),
+                ("t_done", C.c_double), ("nit", C.c_int32), ("nfev", C.c_int32),
+                ("task", C.c_int32), ("warnflag", C.c_int32), ("n_calls", C.c_int32),
+                ("pad", C.c_int32)]
+
 # name -> (restype, argtypes); mirrors include/dhcos.h one to one
 SIGNATURES = {
     "dh_version": (C.c_int, []),
@@ -56,6 +70,11 @@ SIGNATURES = {
     "dh_surface_price_dev": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp, _vp]),
     "dh_surface_loss_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp,
                                       _vp]),
+    "dh_calibrate_lbfgs": (C.c_int, [_vp, _vp, _dp, C.c_int, C.c_double, C.c_double, C.c_int,
+                                     C.c_double, C.POINTER(LbOptions), C.POINTER(LbResult),
+                                     _i32p]),
+    "dh_ctx_set_lb_trace": (C.c_int, [_vp, C.c_int64]),
+    "dh_ctx_read_lb_trace": (C.c_int, [_vp, _dp, C.c_int64, C.POINTER(C.c_int64)]),
     "dh_price_pairs": (C.c_int, [_vp, _dp, _dp, _dp, _i8p, C.c_int64, C.c_int, C.c_double, _dp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
@@ -168,6 +187,19 @@ class Context:
                                              n.value, C.byref(n)))
         return out.reshape(-1, 16)
 
+    def set_lb_trace(self, cap: int):
+        """Diagnostics: record up to cap consumed requests of the next calibrate_lbfgs calls."""
+        _check(load().dh_ctx_set_lb_trace(self._h, int(cap)))
+
+    def read_lb_trace(self):
+        """-> [n, 32] records [start, request, f, x[13], g[13], 0, 0, 0] of the last call."""
+        n = C.c_int64(0)
+        _check(load().dh_ctx_read_lb_trace(self._h, None, 0, C.byref(n)))
+        out = np.zeros((n.value, 32))
+        if n.value:
+            _check(load().dh_ctx_read_lb_trace(self._h, _ptr(out), n.value, C.byref(n)))
+        return out
+
     def synchronize(self):
         _check(load().dh_ctx_synchronize(self._h))
 
@@ -279,6 +311,22 @@ class Surface:
                                           None if prices is None else prices.ctypes.data))
         return sse, bad, prices
 
+    def calibrate_lbfgs(self, x0s, S0, r, N=128, L=10.0, *, maxiter=300, maxfun=15000, maxls=20,
+                        ftol=1e-9, gtol=1e-6, chunk=8):
+        """Device-resident L-BFGS-B for every row of x0s [S, 13] (dh_calibrate_lbfgs).
+        -> (list of LbResult, number of loss launches)."""
+        x0s = _f64(x0s).reshape(-1, 13)
+        S = x0s.shape[0]
+        opt = LbOptions(int(maxiter), int(maxfun), int(maxls), int(chunk), float(ftol),
+                        float(gtol))
+        res = (LbResult * max(S, 1))()
+        nl = C.c_int32(0)
+        with self.ctx._lock:
+            _check(load().dh_calibrate_lbfgs(self.ctx.handle, self._h, _ptr(x0s), S, float(S0),
+                                             float(r), int(N), float(L), C.byref(opt), res,
+                                             C.byref(nl)))
+        return list(res)[:S], nl.value
+
     # device-pointer variants (torch tensors or raw device addresses)
     def price_dev(self, d_params: int, P: int, d_out: int, N=128, L=10.0, stream: int = 0):
         _check(load().dh_surface_price_dev(self.ctx.handle, self._h, _vp(d_params), int(P), int(N),
@@ -308,6 +356,6 @@ def default_context(device: int | None = None) -> Context:
     return ctx
 
 
-__all__ = ["Context", "Surface", "NativeError", "load", "default_context", "device_count",
+__all__ = ["LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "PARAM_STRIDE", "MAX_N", "STRIKE_ABSOLUTE",
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "LIB_PATH", "SIGNATURES"]

@@ -30,6 +30,7 @@ from typing import Dict, List
 import numpy as np
 from scipy.optimize import OptimizeResult, _lbfgsb, minimize
 from scipy.optimize._lbfgsb_py import status_messages, task_messages
+from threadpoolctl import ThreadpoolController
 
 from . import _native
 from .pricer import resolve_call
@@ -253,13 +254,24 @@ class DoubleHestonJumpCalibrator:
         return surf.price(rec, self.N)[0]
 
     def calibrate(self, maxiter: int = 300, multi_start: int = 3, *, lockstep: bool = True,
-                  x0s=None) -> CalibrationResult:
-        """Multi-start L-BFGS-B; returns the best start (strict ``<`` in start order)."""
+                  x0s=None, driver: str = "scipy") -> CalibrationResult:
+        """Multi-start L-BFGS-B; returns the best start (strict ``<`` in start order).
+
+        driver="scipy": SciPy's own setulb on the host, one launch per lockstep request (the
+        reference's optimizer, bit for bit).  driver="device": the device-resident L-BFGS-B
+        (dh_calibrate_lbfgs: the loss launches and the optimizer steps run back to back on the
+        GPU, the host checks for finished starts every few iterations); same algorithm and
+        stopping rules, with the subspace step rounded differently (csrc/dh_lbfgs.h)."""
         start_time = time.time()
         # draw every start's x0 in start order (the only consumer of the global RNG, :256)
         if x0s is None:
             x0s = [self.get_initial_guess(guess_type=s % 3) for s in range(multi_start)]
-        outcomes = run_starts(self, x0s, maxiter, lockstep=lockstep)
+        if driver == "device":
+            outcomes = run_starts_device(self, x0s, maxiter)
+        elif driver == "scipy":
+            outcomes = run_starts(self, x0s, maxiter, lockstep=lockstep)
+        else:
+            raise ValueError(f"driver must be 'scipy' or 'device', not {driver!r}")
         best_result, best_loss = None, np.inf
         for s, out in enumerate(outcomes):
             if out is None:                       # the start raised: except -> continue (:316)
@@ -354,6 +366,20 @@ def lbfgsb_steps(x0, maxiter, maxfun, m=10, ftol=1e-9, gtol=1e-6, maxls=20):
                           status=warnflag, message=msg, x=x, success=(warnflag == 0))
 
 
+_BLAS = None
+
+
+def _single_threaded_blas():
+    """Context that pins the BLAS pools (SciPy's OpenBLAS, which setulb calls on 13-vectors and
+    10x10 blocks) to one thread.  With the default pool (OMP_NUM_THREADS threads) every setulb call
+    pays thread wake-ups worth several times its arithmetic.  Problem sizes are far below
+    OpenBLAS's split thresholds, so the results are the same bits (tests/test_lbfgsb_driver.py)."""
+    global _BLAS
+    if _BLAS is None:
+        _BLAS = ThreadpoolController()
+    return _BLAS.limit(limits=1, user_api="blas")
+
+
 # jac=True: nfev counts one per request, SciPy's FD path counts 14 -> rescale maxfun so the
 # `nfev > maxfun` stop fires at the same request (scipy/_lbfgsb_py.py:466-469)
 _MAXFUN = SCIPY_MAXFUN // (N_PARAMS + 1)
@@ -387,8 +413,17 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
         return outcomes
     gens = [lbfgsb_steps(x0, maxiter, _MAXFUN) for x0 in x0s]
     states = [_StartState() for _ in range(n)]
-    launches = 0
     order = [list(range(n))] if lockstep else [[s] for s in range(n)]
+    with _single_threaded_blas():
+        _advance(cal, gens, states, order, outcomes)
+    last = states[-1]
+    cal.n_calls, cal.best_loss = last.n_calls, last.best_loss   # state after the last start
+    return outcomes
+
+
+def _advance(cal, gens, states, order, outcomes):
+    """run_starts' loop: one launch per lockstep request, setulb steps per start."""
+    launches = 0
     for group in order:
         pending = {}
         for sid in group:
@@ -422,7 +457,34 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
                     del pending[sid]
                 except Exception:      # noqa: BLE001 -- reference: except -> continue
                     del pending[sid]
-    last = states[-1]
-    cal.n_calls, cal.best_loss = last.n_calls, last.best_loss   # state after the last start
+    cal.lockstep_launches = launches
+
+
+def run_starts_device(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int):
+    """run_starts on the device-resident L-BFGS-B (dh_calibrate_lbfgs): every start's requests
+    and optimizer steps run on the GPU; returns [(OptimizeResult, t_done)] in start order.
+    Markets whose loss is constant (an option type of '' -> 1e10, no options -> NaN) have
+    nothing to optimise on the device and take the host driver, which reproduces the
+    reference's result for them."""
+    n = len(x0s)
+    if n == 0:
+        return []
+    surf = cal._get_surface()
+    if surf is None or len(cal.market_options) == 0:
+        return run_starts(cal, x0s, maxiter)
+    t0 = time.time()
+    res, launches = surf.calibrate_lbfgs(np.stack([np.asarray(x, dtype=np.float64)[:N_PARAMS]
+                                                   for x in x0s]),
+                                         cal.spot, cal.risk_free_rate, cal.N, maxiter=maxiter,
+                                         maxfun=_MAXFUN)
+    outcomes = []
+    for r in res:
+        msg = status_messages[r.task // 1000] + ": " + task_messages[r.task % 1000]
+        opt = OptimizeResult(fun=float(r.fun), jac=None, nfev=r.nfev, njev=r.nfev, nit=r.nit,
+                             status=r.warnflag, message=msg, x=np.array(r.x[:]),
+                             success=(r.warnflag == 0))
+        outcomes.append((opt, t0 + r.t_done))
+    cal.n_calls, cal.best_loss = res[-1].n_calls, res[-1].best_loss   # state after the last start
+    cal.loss_evals += sum(r.n_calls for r in res)
     cal.lockstep_launches = launches
     return outcomes

@@ -1,0 +1,126 @@
+// CPU build of the device L-BFGS-B state machine (option-pricing-ffn-lbfgs_amd/csrc/dh_lbfgs.h),
+// for tests only: tests/test_lbfgs_device_algo.py drives it against scipy.optimize.minimize on
+// NumPy objectives, and the GPU tests check the device driver against it.  HVec is the
+// 16-component vector whose dot product sums in the device butterfly's pairwise order, so this
+// build and the step kernel (one component per lane) compute the same bits.  Built by the csrc
+// Makefile (target lbhost) with contraction off, like the device code.
+#include <math.h>
+
+#define DH_HD
+#include "dh_lbfgs.h"
+
+namespace {
+
+using dhlb::kLanes;
+using dhlb::kN;
+
+struct HVec {
+    double v[kLanes];
+};
+
+HVec operator+(const HVec& a, const HVec& b) {
+    HVec o;
+    for (int i = 0; i < kLanes; ++i) o.v[i] = a.v[i] + b.v[i];
+    return o;
+}
+HVec operator-(const HVec& a, const HVec& b) {
+    HVec o;
+    for (int i = 0; i < kLanes; ++i) o.v[i] = a.v[i] - b.v[i];
+    return o;
+}
+HVec operator-(const HVec& a) {
+    HVec o;
+    for (int i = 0; i < kLanes; ++i) o.v[i] = -a.v[i];
+    return o;
+}
+HVec operator*(double s, const HVec& a) {
+    HVec o;
+    for (int i = 0; i < kLanes; ++i) o.v[i] = s * a.v[i];
+    return o;
+}
+// butterfly order: level l adds the partner at distance 2^l (xor); every lane ends with the same
+// value, lane 0's is returned
+double dot(const HVec& a, const HVec& b) {
+    double t[kLanes], u[kLanes];
+    for (int i = 0; i < kLanes; ++i) t[i] = a.v[i] * b.v[i];
+    for (int off = 1; off < kLanes; off <<= 1) {
+        for (int i = 0; i < kLanes; ++i) u[i] = t[i] + t[i ^ off];
+        for (int i = 0; i < kLanes; ++i) t[i] = u[i];
+    }
+    return t[0];
+}
+double amax(const HVec& a) {
+    double m = 0.0;
+    for (int i = 0; i < kLanes; ++i) m = fmax(m, fabs(a.v[i]));
+    return m;
+}
+bool equal(const HVec& a, const HVec& b) {
+    bool e = true;
+    for (int i = 0; i < kLanes; ++i) e = e && (a.v[i] == b.v[i]);
+    return e;
+}
+
+struct HRing {
+    HVec sv[dhlb::kM], yv[dhlb::kM];
+    double drv[dhlb::kM], av[dhlb::kM];
+    const HVec& s(int j) const { return sv[j]; }
+    const HVec& y(int j) const { return yv[j]; }
+    double dr(int j) const { return drv[j]; }
+    double& a(int j) { return av[j]; }
+    void put(int j, const HVec& sj, const HVec& yj, double d) {
+        sv[j] = sj;
+        yv[j] = yj;
+        drv[j] = d;
+    }
+    void shift() {
+        for (int j = 0; j + 1 < dhlb::kM; ++j) {
+            sv[j] = sv[j + 1];
+            yv[j] = yv[j + 1];
+            drv[j] = drv[j + 1];
+        }
+    }
+};
+
+using Core = dhlb::LbCore<HVec, HRing>;
+
+}  // namespace
+
+extern "C" {
+
+int lbh_state_size(void) { return (int)sizeof(Core); }
+
+int lbh_begin(void* st, const double* x0) {
+    Core& c = *(Core*)st;
+    HVec v{};
+    for (int i = 0; i < kN; ++i) v.v[i] = x0[i];
+    return dhlb::lb_begin(c, v);
+}
+
+int lbh_resume(void* st, int maxiter, int maxfun, int maxls, double factr_epsmch, double pgtol) {
+    const dhlb::LbConfig cf{maxiter, maxfun, maxls, 0, factr_epsmch, pgtol};
+    return dhlb::lb_resume(*(Core*)st, cf);
+}
+
+void lbh_point(const void* st, double* x) {
+    const Core& c = *(const Core*)st;
+    for (int i = 0; i < kN; ++i) x[i] = c.xe.v[i];
+}
+
+void lbh_set_fg(void* st, double f, const double* g) {
+    Core& c = *(Core*)st;
+    c.s.fe = f;
+    for (int i = 0; i < kLanes; ++i) c.ge.v[i] = i < kN ? g[i] : 0.0;
+}
+
+// x[13], fun (last evaluated f), and (nit, nfev, task, warnflag)
+void lbh_result(const void* st, double* x, double* fun, int* info) {
+    const Core& c = *(const Core*)st;
+    for (int i = 0; i < kN; ++i) x[i] = c.x.v[i];
+    *fun = c.s.fe;
+    info[0] = c.s.nit;
+    info[1] = c.s.nfev;
+    info[2] = c.s.task;
+    info[3] = c.s.warnflag;
+}
+
+}  // extern "C"

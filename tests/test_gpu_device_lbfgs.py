@@ -1,0 +1,161 @@
+"""GPU tests of the device-resident L-BFGS-B (dh_calibrate_lbfgs, csrc/dh_lbfgs.h): the whole
+multi-start calibration loop runs as loss launches + step launches on the device.
+
+What is asserted, and why (trajectory bits are not a well-posed target: see
+test_gpu_parity.test_calibrate_seed0):
+  * the reference's robust start (guess 0) reproduces its result exactly in kind:
+    ABNORMAL, nit 0, 21 requests (294 loss evaluations), x = x0, fun = the last trial's loss
+    (loss tolerance 1e-9 relative);
+  * calibrate(300, 3, driver="device") under np.random.seed(0) converges below 1e-6 (the
+    reference reaches 1.02e-7), like the SciPy-driven path;
+  * the host loop is an implementation detail: results are bitwise identical for every chunk
+    size (compaction of finished starts and re-emission of their requests) and for every way of
+    batching starts (a start's values depend only on its own x);
+  * the device state machine computes the bits of its CPU build (tests/native/liblbhost.so):
+    replaying the device's own request trace (f, g per request) through the CPU build asks for
+    the same points, bit for bit, and ends with the same x, fun, nit, nfev and stop;
+    (driven instead with losses the host forms itself -- records by NumPy exp / tanh, not the
+    device's ocml ones -- the runs agree only to ~1e-7 after two iterations and separate
+    further: the records' last-bit differences reach the FD gradient amplified by 1 / h = 1e8).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, rel_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dh():
+    import dhcos
+    from dhcos import _native
+    if _native.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return dhcos
+
+
+def _cal(dh, g):
+    return dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+
+
+def test_device_driver_robust_start(dh, calib_golden):
+    from dhcos.calibrator import run_starts_device
+    want = calib_golden["calibrate_seed0_starts"][0]
+    cal = _cal(dh, calib_golden)
+    x0 = np.array(want["x0"])
+    (res, _), = run_starts_device(cal, [x0], 300)
+    assert res.nit == 0 and res.message == want["message"] == "ABNORMAL: "
+    assert res.nfev * 14 == want["nfev"] == 294 and cal.n_calls == want["n_calls"]
+    assert np.array_equal(res.x, x0)
+    assert rel_close(res.fun, want["fun"], 1e-9, 0)
+    assert rel_close(cal.best_loss, want["best_loss"], 1e-6, 0)
+    assert not res.success
+
+
+def test_device_driver_calibrate_seed0(dh, calib_golden):
+    np.random.seed(0)
+    cal = _cal(dh, calib_golden)
+    r = cal.calibrate(maxiter=300, multi_start=3, driver="device")
+    assert r.success and r.message.startswith("CONVERGENCE")
+    assert r.final_loss < 1e-6
+    assert rel_close(r.model_prices, cal.market_prices, 5e-3, 0).all()
+    assert 0 < r.calibration_time < 5.0
+    assert cal.lockstep_launches > 0
+
+
+def _starts(g, n, seed=3):
+    rs = np.random.RandomState(seed)
+    base = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
+    return np.stack([base[i % 3] + (0.0 if i < 3 else 0.05) * rs.randn(13) for i in range(n)])
+
+
+def _same(a, b):
+    for ra, rb in zip(a, b):
+        assert np.array_equal(np.array(ra.x[:]), np.array(rb.x[:]))
+        assert ra.fun == rb.fun and ra.nit == rb.nit and ra.nfev == rb.nfev
+        assert ra.task == rb.task and ra.n_calls == rb.n_calls and ra.best_loss == rb.best_loss
+
+
+def test_chunk_size_and_batching_invariance(dh, calib_golden):
+    cal = _cal(dh, calib_golden)
+    surf = cal._get_surface()
+    x0s = _starts(calib_golden, 6)
+    ref, _ = surf.calibrate_lbfgs(x0s, 100.0, 0.05, 128, maxiter=40, chunk=8)
+    for chunk in (1, 3):
+        got, _ = surf.calibrate_lbfgs(x0s, 100.0, 0.05, 128, maxiter=40, chunk=chunk)
+        _same(got, ref)
+    alone = [surf.calibrate_lbfgs(x0s[i:i + 1], 100.0, 0.05, 128, maxiter=40, chunk=5)[0][0]
+             for i in range(len(x0s))]
+    _same(alone, ref)
+    tasks = {r.task for r in ref}
+    assert tasks <= {4401, 4402, 5504, 8000}, tasks
+
+
+def test_maxiter_stop(dh, calib_golden):
+    cal = _cal(dh, calib_golden)
+    surf = cal._get_surface()
+    x0 = _starts(calib_golden, 2)[1:2]
+    (r,), _ = surf.calibrate_lbfgs(x0, 100.0, 0.05, 128, maxiter=3)
+    assert r.nit == 3 and r.task == 5504 and r.warnflag == 1
+
+
+def test_device_replays_bitwise_on_cpu_build(dh, calib_golden):
+    import test_lbfgs_device_algo as T
+    lib = C.CDLL(os.path.join(ROOT, "tests", "native", "liblbhost.so"))
+    lib.lbh_begin.argtypes = [C.c_void_p, T._D]
+    lib.lbh_point.argtypes = [C.c_void_p, T._D]
+    lib.lbh_set_fg.argtypes = [C.c_void_p, C.c_double, T._D]
+    lib.lbh_resume.argtypes = [C.c_void_p] + [C.c_int] * 3 + [C.c_double] * 2
+    lib.lbh_result.argtypes = [C.c_void_p, T._D, T._D, C.POINTER(C.c_int)]
+    cal = _cal(dh, calib_golden)
+    surf = cal._get_surface()
+    x0s = _starts(calib_golden, 5)
+    surf.ctx.set_lb_trace(100000)
+    try:
+        res, _ = surf.calibrate_lbfgs(x0s, 100.0, 0.05, 128, maxiter=300, maxfun=1071)
+        tr = surf.ctx.read_lb_trace()
+    finally:
+        surf.ctx.set_lb_trace(0)
+    assert len(tr) == sum(r.n_calls for r in res) // 14
+    eps = np.finfo(float).eps
+    for s, r in enumerate(res):
+        rows = tr[tr[:, 0] == s]
+        rows = rows[np.argsort(rows[:, 1])]
+        assert np.array_equal(rows[:, 1], np.arange(len(rows)))
+        st = C.create_string_buffer(lib.lbh_state_size())
+        x0 = np.ascontiguousarray(x0s[s])
+        more = lib.lbh_begin(st, x0.ctypes.data_as(T._D))
+        xe = np.empty(13)
+        k = 0
+        while more:
+            lib.lbh_point(st, xe.ctypes.data_as(T._D))
+            assert np.array_equal(xe, rows[k, 3:16]), (s, k)
+            g = np.ascontiguousarray(rows[k, 16:29])
+            lib.lbh_set_fg(st, rows[k, 2], g.ctypes.data_as(T._D))
+            more = lib.lbh_resume(st, 300, 1071, 20, (1e-9 / eps) * eps, 1e-6)
+            k += 1
+        assert k == len(rows) == r.nfev
+        x = np.empty(13)
+        fv = C.c_double()
+        info = (C.c_int * 4)()
+        lib.lbh_result(st, x.ctypes.data_as(T._D), C.byref(fv), info)
+        assert np.array_equal(x, np.array(r.x[:])) and fv.value == r.fun
+        assert list(info) == [r.nit, r.nfev, r.task, r.warnflag]
+
+
+def test_degenerate_markets_fall_back_to_reference_semantics(dh, calib_golden):
+    """'' option type (every loss 1e10) and an empty market (NaN) have nothing to optimise; the
+    device driver hands them to the host driver and returns the reference's result."""
+    mkt = [dict(o) for o in calib_golden["test_market"]]
+    mkt[0]["option_type"] = ""
+    for market in (mkt, []):
+        r = dh.DoubleHestonJumpCalibrator(100.0, 0.05, market).calibrate(
+            maxiter=10, multi_start=1, driver="device")
+        h = dh.DoubleHestonJumpCalibrator(100.0, 0.05, market).calibrate(maxiter=10, multi_start=1)
+        assert (r.final_loss, r.success, r.message, r.iterations) == \
+            (h.final_loss, h.success, h.message, h.iterations)
+    assert not r.success

@@ -21,27 +21,32 @@ from dhcos.calibrator import DoubleHestonJumpCalibrator  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
+    ap.add_argument("--driver", default="scipy", choices=["scipy", "device"])
+    ap.add_argument("--starts", type=int, default=3)
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     opts, S0, r = bench.make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
     for _ in range(2):                      # warm-up (surface upload, JIT of nothing, caches)
         np.random.seed(0)
-        DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"]).calibrate(300, 3)
+        DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"]).calibrate(300, args.starts, driver=args.driver)
     times = []
     for _ in range(7):
         cal = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"])
         np.random.seed(0)
         t0 = time.perf_counter()
-        cal.calibrate(300, 3)
+        cal.calibrate(300, args.starts, driver=args.driver)
         times.append(time.perf_counter() - t0)
     t_plain = float(np.median(times))
     cal = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"])
     np.random.seed(0)
     pr = cProfile.Profile()
     pr.enable()
-    cal.calibrate(300, 3)
+    cal.calibrate(300, args.starts, driver=args.driver)
     pr.disable()
-    print(f"calibrate(300, 3): median of 7 {t_plain * 1e3:.2f} ms (min {min(times) * 1e3:.2f}), "
+    np.random.seed(0)
+    res = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"]).calibrate(300, args.starts, driver=args.driver)
+    print(f"{args.driver} driver: final loss {res.final_loss:.6e} nit {res.iterations} {res.message}")
+    print(f"calibrate(300, {args.starts}): median of 7 {t_plain * 1e3:.2f} ms (min {min(times) * 1e3:.2f}), "
           f"{cal.lockstep_launches} launches, "
           f"{t_plain / cal.lockstep_launches * 1e6:.1f} us per launch")
     pstats.Stats(pr).sort_stats("tottime").print_stats(18)
