@@ -185,6 +185,10 @@ CONFIGS = {
     "c3": dict(nK=100, nT=100, N=512, starts=3, put_itm=True,
                workload="10,000-option surface (100 K/S x 100 T, puts K<S), N=512, 3 lockstep "
                         "starts x 14 param sets per step"),
+    "c4": dict(nK=32, nT=32, N=256, starts=64, put_itm=False, strong=True,
+               workload="64 multi-start calibrations of the 1,024-option surface (32 K/S x 32 T), "
+                        "N=256: one lockstep function+gradient request of every start's 14 param "
+                        "sets per step, the 64 starts sharded over the GPUs"),
     "c1": dict(nK=5, nT=3, N=128, starts=1, put_itm=False,
                workload="15-option grid (5 K x 3 T), N=128, one function+gradient request"),
     "c5": dict(gen=True, P=1_000_000, N=128,
@@ -192,6 +196,32 @@ CONFIGS = {
                         "calls (8 K/S in linspace(0.8, 1.2) of each sample's spot x T in "
                         "{0.25, 0.5, 1, 2}), N=128, priced in one pass per step"),
 }
+
+
+def calib_leg(S0, r, opts, N, n_starts, world, coll, driver):
+    """Time calibrate(maxiter=300, multi_start=n_starts) under np.random.seed(0) (starts
+    sharded over the ranks at N > 1) with the given optimizer driver; max over ranks."""
+    cal = DoubleHestonJumpCalibrator(S0, r, opts, N=N)
+    if world > 1:
+        dist.barrier()
+    np.random.seed(0)
+    t0 = time.perf_counter()
+    if world > 1:
+        res = calibrate_sharded(cal, maxiter=300, multi_start=n_starts, driver=driver)
+    else:
+        res = cal.calibrate(maxiter=300, multi_start=n_starts, driver=driver)
+    tc = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([tc], dtype=torch.float64, device=coll)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tc = float(tt.item())
+    return {"driver": driver, "calibrations_per_sec": 1.0 / tc, "starts_per_sec": n_starts / tc,
+            "seconds": tc, "starts": n_starts, "iterations": int(res.iterations),
+            "final_loss": float(res.final_loss), "message": res.message,
+            "lockstep_launches_rank0": int(getattr(cal, "lockstep_launches", 0)),
+            "loss_evals_rank0": int(cal.loss_evals),
+            "calibrate": f"calibrate(maxiter=300, multi_start={n_starts}, driver='{driver}'), "
+                         "np.random.seed(0)" + (", starts sharded over ranks" if world > 1 else "")}
 
 
 def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
@@ -337,9 +367,12 @@ def main():
     M = len(opts)
     cal = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"])
     surf = cal._get_surface()
-    S = 14 * cfg["starts"]
+    # c4 deals its 64 starts over the ranks (strong scaling); the others run a fixed request per
+    # rank (weak scaling)
+    starts_rank = -(-cfg["starts"] // world) if cfg.get("strong") else cfg["starts"]
+    S = 14 * starts_rank
     K_, W_ = args.steps, args.warmup
-    host = step_params(cal, K_ + W_, cfg["starts"], seed=100 + rank)
+    host = step_params(cal, K_ + W_, starts_rank, seed=100 + rank)
     d_params = torch.from_numpy(host).to(dev)
     d_sse = torch.empty((K_ + W_, S), dtype=torch.float64, device=dev)
     d_bad = torch.empty((K_ + W_, S), dtype=torch.int32, device=dev)
@@ -416,38 +449,22 @@ def main():
                                       "achieved_TFLOPs": survey_flop / (ker_ms * 1e-3) / 1e12}}
 
     # ---- calibrations/sec: one full calibration of the same surface; at N > 1 its starts are
-    # sharded over the ranks (dhcos.distributed, 3 starts per GPU: weak scaling) ----
-    calib = None
+    # sharded over the ranks (dhcos.distributed; 3 starts per GPU, weak scaling; c4: 64 starts
+    # in all, strong scaling).  Two optimizer drivers: SciPy's setulb on the host (the reference's
+    # optimizer bit for bit, one launch + one host round trip per lockstep request) and the
+    # device-resident L-BFGS-B (dh_calibrate_lbfgs) ----
+    calib = calib_dev = None
     if not args.no_calib:
-        c2 = DoubleHestonJumpCalibrator(S0, r, opts, N=N)
-        n_starts = 3 * world
-        if world > 1:
-            dist.barrier()
-        np.random.seed(0)
-        t0 = time.perf_counter()
-        if world > 1:
-            res = calibrate_sharded(c2, maxiter=300, multi_start=n_starts)
-        else:
-            res = c2.calibrate(maxiter=300, multi_start=n_starts)   # reference defaults
-        tc = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([tc], dtype=torch.float64, device=coll)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            tc = float(tt.item())
-        calib = {"calibrations_per_sec": 1.0 / tc, "starts_per_sec": n_starts / tc,
-                 "seconds": tc, "starts": n_starts, "iterations": int(res.iterations),
-                 "final_loss": float(res.final_loss), "message": res.message,
-                 "lockstep_launches_rank0": int(getattr(c2, "lockstep_launches", 0)),
-                 "loss_evals_rank0": int(c2.loss_evals),
-                 "calibrate": f"calibrate(maxiter=300, multi_start={n_starts}), np.random.seed(0)"
-                              + (", starts sharded over ranks" if world > 1 else "")}
+        n_starts = cfg["starts"] if cfg.get("strong") else 3 * world
+        calib = calib_leg(S0, r, opts, N, n_starts, world, coll, "scipy")
+        calib_dev = calib_leg(S0, r, opts, N, n_starts, world, coll, "device")
 
     if rank == 0:
         line = {
             "metric": "option-prices/sec (COS, calibration objective) + calibrations/sec",
             "value": value, "unit": "option-prices/s", "n_gpus": world, "steps": K_,
             "warmup": W_, "ms_per_step": dt / K_ * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": "strong" if cfg.get("strong") else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": cfg["workload"], "options": M, "cos_terms": N,
                        "param_sets_per_step": S, "prices_per_step": prices_per_step,
                        "parallelism": f"independent requests per rank x{world}"},
@@ -456,14 +473,16 @@ def main():
         }
         if calib:
             line["calibration"] = calib
+            line["calibration_device"] = calib_dev
         if cpu:
             line["cpu_baseline"] = cpu
             line["speedup_vs_cpu"] = value / cpu["value"]
             if calib and world == 1:
                 # the same calibration on the CPU port: every loss evaluation prices M options
-                cpu_s = calib["loss_evals_rank0"] * M / line["cpu_baseline"]["value"]
-                calib["cpu_port_seconds_extrapolated"] = cpu_s
-                calib["speedup_vs_cpu"] = cpu_s / calib["seconds"]
+                for c in (calib, calib_dev):
+                    cpu_s = c["loss_evals_rank0"] * M / line["cpu_baseline"]["value"]
+                    c["cpu_port_seconds_extrapolated"] = cpu_s
+                    c["speedup_vs_cpu"] = cpu_s / c["seconds"]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -2165,17 +2165,17 @@ __device__ __forceinline__ double dot(WaveVec a, WaveVec b) { return row_sum(a.v
 __device__ __forceinline__ double amax(WaveVec a) { return fmax(0.0, row_max(fabs(a.v))); }
 __device__ __forceinline__ bool equal(WaveVec a, WaveVec b) { return __all(a.v == b.v); }
 
-// The pair memory in LDS: s_j, y_j as 16-double rows (lane i reads column i), dr_j and the
+// The pair memory in LDS: s_j, y_j as 16-double rows (lane i reads column i), rho_j and the
 // two-loop's alpha_j.  Every lane computes the same scalars, so the scalar writes are uniform.
 struct WaveRing {
     double* rs;                // [kM][16]
     double* ry;                // [kM][16]
-    double* rdr;               // [kM]
+    double* rdr;               // [kM] rho_j = 1 / dr_j
     double* ra;                // [kM]
     int lane;
     __device__ WaveVec s(int j) const { return {lane < dhlb::kLanes ? rs[j * dhlb::kLanes + lane] : 0.0}; }
     __device__ WaveVec y(int j) const { return {lane < dhlb::kLanes ? ry[j * dhlb::kLanes + lane] : 0.0}; }
-    __device__ double dr(int j) const { return rdr[j]; }
+    __device__ double rho(int j) const { return rdr[j]; }
     __device__ double& a(int j) { return ra[j]; }
     __device__ void put(int j, WaveVec sj, WaveVec yj, double d) {
         if (lane < dhlb::kLanes) {
@@ -2203,7 +2203,7 @@ constexpr int kLbTrace = 32;
 // Global state of one start: the vectors as 16-double rows (lane i holds column i), the pair
 // memory (staged in LDS by the step kernel), then the scalars.
 constexpr int kLbVecs = 10;                           // x g z d t r xe ge dx pen
-constexpr int kLbRing = 2 * dhlb::kM * dhlb::kLanes + dhlb::kM;   // s rows, y rows, dr
+constexpr int kLbRing = 2 * dhlb::kM * dhlb::kLanes + dhlb::kM;   // s rows, y rows, rho
 struct LbSlot {
     double vec[kLbVecs][dhlb::kLanes];
     double ring[kLbRing];

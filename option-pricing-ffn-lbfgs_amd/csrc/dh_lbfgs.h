@@ -5,8 +5,8 @@
 // xor butterflies over 16 lanes), the CPU check build (tests/native/lb_host.cpp) with a plain
 // 16-double array whose dot product sums in the same pairwise order -- so both give the same
 // bits.  V provides +, -, * (elementwise), double * V, dot(a, b), amax(a), equal(a, b).  The
-// pair memory is a separate type R (LDS-resident on the device) with s(j), y(j), dr(j), a(j)
-// (the two-loop's alpha scratch), put(j, s, y, dr) and shift() (drop the oldest pair).
+// pair memory is a separate type R (LDS-resident on the device) with s(j), y(j), rho(j) (1 / dr),
+// a(j) (the two-loop's alpha scratch), put(j, s, y, rho) and shift() (drop the oldest pair).
 //
 // What it restates (SciPy 1.15.3, the optimizer the reference calls at lbfgs_calibrator.py:259-269
 // as minimize(method='L-BFGS-B', options={maxiter, ftol: 1e-9, gtol: 1e-6}) without bounds):
@@ -26,7 +26,7 @@
 //     with ftol = 1e-3, gtol = 0.9, xtol = 0.1, stpmin = 0 (as in scipy/optimize/_dcsrch.py).
 // What differs: the subspace step B^-1 (-g) of the compact representation (formk / subsm with
 // every variable free) is formed by the two-loop recursion over the same pairs (s_i, y_i), the
-// same theta and the same s_i'y_i (= dr), which is the same matrix (Byrd, Nocedal and Schnabel,
+// same theta and rho_i = 1 / dr (dr = L-BFGS-B's s_i'y_i), which is the same matrix (Byrd, Nocedal and Schnabel,
 // 1994) rounded differently.  Dot products are pairwise (butterfly) sums of rounded products,
 // and nothing is contracted into FMAs, so the host and device builds give the same bits.  The
 // pairs are kept oldest-first in slots 0..col-1 (shifted down when the memory is full) instead of
@@ -88,7 +88,7 @@ template <class V, class R>
 struct LbCore {
     V x, g, z, d, t, r;          // mainlb vectors
     V xe, ge;                    // ScalarFunction: last evaluated point and gradient
-    R pairs;                     // (s_i, y_i, s_i'y_i = L-BFGS-B's dr at the update), oldest first
+    R pairs;                     // (s_i, y_i, 1 / dr_i with dr = L-BFGS-B's s_i'y_i), oldest first
     LbScalars s;
 };
 
@@ -265,13 +265,13 @@ DH_HD inline void subspace_step(LbCore<V, R>& c) {
     R& m = c.pairs;
     V q = -c.g;
     for (int j = c.s.col - 1; j >= 0; --j) {           // newest -> oldest
-        const double a = dot(m.s(j), q) / m.dr(j);
+        const double a = m.rho(j) * dot(m.s(j), q);
         m.a(j) = a;
         q = q - a * m.y(j);
     }
     q = (1.0 / c.s.theta) * q;
     for (int j = 0; j < c.s.col; ++j) {                // oldest -> newest
-        const double b = dot(m.y(j), q) / m.dr(j);
+        const double b = m.rho(j) * dot(m.y(j), q);
         q = q + (m.a(j) - b) * m.s(j);
     }
     c.z = c.x + q;
@@ -416,7 +416,7 @@ L777:
     s.iupdat += 1;                                 // matupd
     if (s.col == kM) c.pairs.shift();              // drop the oldest pair
     else s.col += 1;
-    c.pairs.put(s.col - 1, c.d, c.r, dr);
+    c.pairs.put(s.col - 1, c.d, c.r, 1.0 / dr);
     s.theta = rr / dr;
     goto L222;
 }

@@ -27,7 +27,8 @@ import torch
 import torch.distributed as dist
 
 from . import _native
-from .calibrator import (CalibrationResult, DoubleHestonJumpCalibrator, N_PARAMS, run_starts)
+from .calibrator import (CalibrationResult, DoubleHestonJumpCalibrator, N_PARAMS, run_starts,
+                         run_starts_device)
 
 _MSG_BYTES = 64                        # SciPy messages are <= 52 characters
 _REC = 7 + N_PARAMS                    # status, start, fun, success, nit, nfev, t_rel, x[13]
@@ -113,19 +114,22 @@ def gather_start_records(local, n_starts, group=None):
 
 
 def calibrate_sharded(cal: DoubleHestonJumpCalibrator, maxiter: int = 300, multi_start: int = 3,
-                      *, group=None, x0s=None) -> CalibrationResult:
-    """``cal.calibrate(maxiter, multi_start)`` with the starts sharded over the process group.
-    Every rank returns the same ``CalibrationResult``."""
+                      *, group=None, x0s=None, driver: str = "scipy") -> CalibrationResult:
+    """``cal.calibrate(maxiter, multi_start, driver=driver)`` with the starts sharded over the
+    process group.  Every rank returns the same ``CalibrationResult``."""
     rank, world = _world(group)
     if world == 1:
-        return cal.calibrate(maxiter=maxiter, multi_start=multi_start, x0s=x0s)
+        return cal.calibrate(maxiter=maxiter, multi_start=multi_start, x0s=x0s, driver=driver)
+    if driver not in ("scipy", "device"):
+        raise ValueError(f"driver must be 'scipy' or 'device', not {driver!r}")
     t0 = time.time()
     if x0s is None and rank == 0:
         x0s = [cal.get_initial_guess(guess_type=s % 3) for s in range(multi_start)]
     x0s = _broadcast_f64(None if x0s is None else np.asarray(x0s), (multi_start, N_PARAMS),
                          group)
     mine = start_shard(multi_start, rank, world)
-    outcomes = run_starts(cal, [x0s[s] for s in mine], maxiter) if mine else []
+    run = run_starts_device if driver == "device" else run_starts
+    outcomes = run(cal, [x0s[s] for s in mine], maxiter) if mine else []
     local = [_encode(s, o, t0) for s, o in zip(mine, outcomes)]
     table = gather_start_records(local, multi_start, group)
 

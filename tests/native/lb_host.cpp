@@ -65,7 +65,7 @@ struct HRing {
     double drv[dhlb::kM], av[dhlb::kM];
     const HVec& s(int j) const { return sv[j]; }
     const HVec& y(int j) const { return yv[j]; }
-    double dr(int j) const { return drv[j]; }
+    double rho(int j) const { return drv[j]; }
     double& a(int j) { return av[j]; }
     void put(int j, const HVec& sj, const HVec& yj, double d) {
         sv[j] = sj;
