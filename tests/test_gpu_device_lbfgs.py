@@ -159,3 +159,42 @@ def test_degenerate_markets_fall_back_to_reference_semantics(dh, calib_golden):
         assert (r.final_loss, r.success, r.message, r.iterations) == \
             (h.final_loss, h.success, h.message, h.iterations)
     assert not r.success
+
+
+def _sharded_worker(rank, world, port, out_dir, market):
+    import pickle
+    import torch.distributed as dist
+    import dhcos
+    from dhcos import distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        np.random.seed(0 if rank == 0 else 4321 + rank)     # x0s are drawn on rank 0
+        cal = dhcos.DoubleHestonJumpCalibrator(100.0, 0.05, market)
+        res = D.calibrate_sharded(cal, maxiter=300, multi_start=4, driver="device")
+        with open(os.path.join(out_dir, f"rank{rank}.pkl"), "wb") as fh:
+            pickle.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_device_driver_equals_single_process(dh, calib_golden, tmp_path):
+    """Two ranks (gloo) sharing the GPU, each running its starts on the device driver, return
+    the single-process result bit for bit (a start's trajectory does not depend on which starts
+    share its launches)."""
+    import pickle
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    market = calib_golden["test_market"]
+    mp.spawn(_sharded_worker, args=(2, port, str(tmp_path), market), nprocs=2, join=True)
+    np.random.seed(0)
+    want = dh.DoubleHestonJumpCalibrator(100.0, 0.05, market).calibrate(300, 4, driver="device")
+    for r in range(2):
+        got = pickle.load(open(tmp_path / f"rank{r}.pkl", "rb"))
+        assert got.final_loss == want.final_loss and got.iterations == want.iterations
+        assert got.message == want.message and got.parameters == want.parameters
+        np.testing.assert_array_equal(got.model_prices, want.model_prices)

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--mode", default="loss")
     ap.add_argument("--path", type=int, default=0, help="0 auto, 1 split, 2 fused")
     ap.add_argument("--dump", default="", help="save the raw [blocks, 8] stamps (.npy)")
+    ap.add_argument("--dev", action="store_true",
+                    help="params / outputs in device memory (loss_dev), as the bench and the "
+                         "device L-BFGS driver run; default: the host API (zero-copy params)")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     opts, S0, r = bench.make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
@@ -38,8 +41,20 @@ def main():
     for _ in range(3):
         surf.loss_terms(host[0], cfg["N"])
     surf.ctx.set_path(args.path)
+    if args.dev:
+        d_p = torch.from_numpy(np.ascontiguousarray(host[1])).cuda()
+        d_sse = torch.empty(d_p.shape[0], dtype=torch.float64, device="cuda")
+        d_bad = torch.empty(d_p.shape[0], dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        for _ in range(3):
+            surf.loss_dev(d_p.data_ptr(), d_p.shape[0], d_sse.data_ptr(), d_bad.data_ptr(),
+                          N=cfg["N"])
+        surf.ctx.synchronize()
     surf.ctx.debug_stamps(True)
-    if args.mode == "loss":
+    if args.dev:
+        surf.loss_dev(d_p.data_ptr(), d_p.shape[0], d_sse.data_ptr(), d_bad.data_ptr(), N=cfg["N"])
+        surf.ctx.synchronize()
+    elif args.mode == "loss":
         surf.loss_terms(host[1], cfg["N"])
     else:
         surf.price(host[1], cfg["N"])
