@@ -66,10 +66,10 @@ void* dh_ctx_stream(dh_ctx* ctx);
  * operation order (own CF and sincos per COS term) instead of the shared-table fast path.   */
 int dh_ctx_set_exact(dh_ctx* ctx, int on);
 /* Request kernels of the fast path.  AUTO (default): one fused launch per request when every
- * maturity group fits one tile (<= 256 options) and the request has at most 1,024 (param set,
- * maturity) tables (latency-bound calibration requests), else a COS-table launch then an option
- * launch.  FUSED / SPLIT force one of the two where it
- * applies.  Both produce the same bits; the choice only changes speed.                      */
+ * maturity group fits one tile (<= 256 options), except small tiles in large calls (generator
+ * grids: a COS-table launch then the lane-per-option-group kernel); otherwise the table launch
+ * then an option launch.  FUSED / SPLIT force one of the two where it applies.  Both produce
+ * the same bits; the choice only changes speed.                                              */
 enum { DH_PATH_AUTO = 0, DH_PATH_SPLIT = 1, DH_PATH_FUSED = 2 };
 int dh_ctx_set_path(dh_ctx* ctx, int path);
 /* DH_PATH_FUSED or DH_PATH_SPLIT: the kernels the last fast-path request ran (0 before any). */
@@ -156,9 +156,10 @@ typedef struct {
 int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double* x0, int S, double S0,
                        double r, int N, double L, const dh_lb_options* opt, dh_lb_result* out,
                        int32_t* n_launches);
-/* Diagnostics (tests): with cap > 0, dh_calibrate_lbfgs records every consumed request as 32
- * doubles [start, request number, f, x[13], g[13], 0 0 0] (order across starts arbitrary);
- * dh_ctx_read_lb_trace copies up to cap records of the last call and sets *n to the count.     */
+/* Diagnostics (tests): with cap > 0, dh_calibrate_lbfgs records every consumed request as 40
+ * doubles [start, request number, f, x[13], g[13], 0 0 0, 6 phase stamps of the step kernel
+ * (DH_STAMPS build only, else 0) 0 0] (order across starts arbitrary); dh_ctx_read_lb_trace
+ * copies up to cap records of the last call and sets *n to the count.                         */
 int dh_ctx_set_lb_trace(dh_ctx* ctx, int64_t cap);
 int dh_ctx_read_lb_trace(dh_ctx* ctx, double* out, int64_t cap, int64_t* n);
 

@@ -1464,7 +1464,6 @@ int launch_exact(dh_ctx* ctx, const PriceArgs& A, hipStream_t st) {
     return DH_OK;
 }
 
-constexpr int64_t kFusedMaxTables = 1024;   // auto path: fused up to this many (p, g) tables
 constexpr int kZeroCopyMaxSets = 1024;       // host-API loss requests up to this many param sets
                                              // read / write through mapped host memory
 
@@ -1516,11 +1515,11 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         const bool small_call = max_nopt <= kSmallTile && A0.P * tasks_per_p >= kSmallMinTasks;
         const bool fusable = (A0.paired || A0.max_group <= kTileMax) &&
                              fused_lds_bytes(N, A0.opt_cap) <= (size_t)kLdsDyn;
-        // auto: fused while the request is latency-bound (few tables); large requests keep the
-        // two launches, whose table kernel runs at its own occupancy
-        const bool few = A0.P * (A0.paired ? 1 : A0.n_groups) <= kFusedMaxTables;
+        // auto: fused wherever it applies except small tiles in large calls (generator grids,
+        // whose lane-per-option-group kernel is 1.7x faster); measured on the current kernels:
+        // C3 113 vs 133 us, C4 393 vs 407 us per request
         const bool fused = fusable && (ctx->path == DH_PATH_FUSED ||
-                                       (ctx->path == DH_PATH_AUTO && !small_call && few));
+                                       (ctx->path == DH_PATH_AUTO && !small_call));
         ctx->last_path = fused ? DH_PATH_FUSED : DH_PATH_SPLIT;
         if (fused) return launch_fused(ctx, A0, st);
     }
@@ -2197,8 +2196,21 @@ struct WaveRing {
 
 using WaveCore = dhlb::LbCore<WaveVec, WaveRing>;
 
-// diagnostic trace record of one consumed request: start, request number, f, x[13], g[13]
-constexpr int kLbTrace = 32;
+// diagnostic trace record of one consumed request: start, request number, f, x[13], g[13], 3 spare,
+// then (DH_STAMPS build only) s_memtime at the step kernel's phase boundaries: start, state
+// loaded, request consumed, state machine done, request emitted, end
+constexpr int kLbTrace = 40;
+constexpr int kLbStamp0 = 32;
+
+__device__ __forceinline__ unsigned long long lb_clock() {
+#ifdef DH_STAMPS
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+#else
+    return 0;
+#endif
+}
 
 // Global state of one start: the vectors as 16-double rows (lane i holds column i), the pair
 // memory (staged in LDS by the step kernel), then the scalars.
@@ -2287,14 +2299,18 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     __shared__ double ring[kLbRing + dhlb::kM];
     __shared__ double fl[dhlb::kLanes];
     __shared__ double pb[dhlb::kLanes], pp[dhlb::kLanes];
+    const unsigned long long t_start = lb_clock();
     const int slot = blockIdx.x;
     const int lane = threadIdx.x;
     const int sidx = A.live[slot];
     LbSlot* G = A.states + sidx;
     WaveCore c;
+    unsigned long long t_load = 0, t_req = 0, t_sm = 0;
     c.pairs = WaveRing{ring, ring + dhlb::kM * dhlb::kLanes, ring + 2 * dhlb::kM * dhlb::kLanes,
                        ring + kLbRing, lane};
     WaveVec dx, pen;
+    double req_sse = 0.0;
+    int req_bad = 0;
     if (A.mode == 0) {
         c.s = dhlb::LbScalars{};
         const WaveVec z{0.0};
@@ -2305,9 +2321,25 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
         c.s.best_loss = __builtin_huge_val();
         c.s.n_calls = 0;
     } else {
+        // every load is issued before any is used (one memory round trip): the finished request's
+        // loss terms, the pair memory, the vectors and the scalars
+        if (A.mode == 1 && lane < dhlb::kPts) {
+            const size_t i = (size_t)slot * dhlb::kPts + lane;
+            req_sse = A.sse[i];
+            req_bad = A.bad[i];
+        }
+        double rg[(kLbRing + 63) / 64];
+#pragma unroll
+        for (int j = 0; j < (kLbRing + 63) / 64; ++j) {
+            const int i = lane + 64 * j;
+            rg[j] = i < kLbRing ? G->ring[i] : 0.0;
+        }
         c.s = G->s;
-        if (c.s.done) return;                          // uniform across the wave
-        for (int i = lane; i < kLbRing; i += 64) ring[i] = G->ring[i];
+#pragma unroll
+        for (int j = 0; j < (kLbRing + 63) / 64; ++j) {
+            const int i = lane + 64 * j;
+            if (i < kLbRing) ring[i] = rg[j];
+        }
         c.x = lb_ld(G, 0, lane);
         c.g = lb_ld(G, 1, lane);
         c.z = lb_ld(G, 2, lane);
@@ -2318,14 +2350,14 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
         c.ge = lb_ld(G, 7, lane);
         dx = lb_ld(G, 8, lane);
         pen = lb_ld(G, 9, lane);
+        if (c.s.done) return;                          // uniform across the wave
     }
     int need = 1;
+    double* tr = nullptr;                              // this request's trace record, if any
     if (A.mode == 1) {
+        t_load = lb_clock();
         double f = __builtin_huge_val();
-        if (lane < dhlb::kPts) {
-            const size_t i = (size_t)slot * dhlb::kPts + lane;
-            f = A.bad[i] > 0 ? kInvalidLoss : A.sse[i] / (double)A.M + pen.v;
-        }
+        if (lane < dhlb::kPts) f = req_bad > 0 ? kInvalidLoss : req_sse / (double)A.M + pen.v;
         if (lane < dhlb::kLanes) fl[lane] = f;
         __syncthreads();
         const double lo = row_min((f == f && f != kInvalidLoss) ? f : __builtin_huge_val());
@@ -2338,7 +2370,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
             if (lane == 0) k = atomicAdd(A.trace_n, 1ull);
             k = __shfl(k, 0, 64);
             if ((int64_t)k < A.trace_cap) {
-                double* tr = A.trace + k * kLbTrace;
+                tr = A.trace + k * kLbTrace;
                 if (lane == 0) {
                     tr[0] = sidx;
                     tr[1] = c.s.n_calls / dhlb::kPts - 1;
@@ -2353,7 +2385,9 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     }
     __syncthreads();
     if (A.mode == 1) {
+        t_req = lb_clock();
         need = dhlb::lb_resume(c, A.cfg);
+        t_sm = lb_clock();
         if (!need && lane == 0) {
             __hip_atomic_store(&A.done[sidx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             atomicSub(A.live_count, 1);
@@ -2361,6 +2395,8 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     }
     if (need) lb_emit(c, dx, pen, pb, pp, A, slot, lane);
     __syncthreads();
+    const unsigned long long t_emit = lb_clock();
+    (void)t_emit;
     for (int i = lane; i < kLbRing; i += 64) G->ring[i] = ring[i];
     lb_st(G, 0, lane, c.x);
     lb_st(G, 1, lane, c.g);
@@ -2373,6 +2409,13 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     lb_st(G, 8, lane, dx);
     lb_st(G, 9, lane, pen);
     if (lane == 0) G->s = c.s;
+#ifdef DH_STAMPS
+    if (tr && lane == 0) {
+        const unsigned long long t_end = lb_clock();
+        const unsigned long long ts[6] = {t_start, t_load, t_req, t_sm, t_emit, t_end};
+        for (int i = 0; i < 6; ++i) tr[kLbStamp0 + i] = (double)ts[i];
+    }
+#endif
 }
 
 int launch_lb_step(hipStream_t st, const LbArgs& A, int n_live) {

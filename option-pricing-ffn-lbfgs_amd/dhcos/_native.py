@@ -192,10 +192,11 @@ class Context:
         _check(load().dh_ctx_set_lb_trace(self._h, int(cap)))
 
     def read_lb_trace(self):
-        """-> [n, 32] records [start, request, f, x[13], g[13], 0, 0, 0] of the last call."""
+        """-> [n, 40] records [start, request, f, x[13], g[13], 0, 0, 0, stamps[6], 0, 0] of the
+        last call (stamps only in the DH_STAMPS build)."""
         n = C.c_int64(0)
         _check(load().dh_ctx_read_lb_trace(self._h, None, 0, C.byref(n)))
-        out = np.zeros((n.value, 32))
+        out = np.zeros((n.value, 40))
         if n.value:
             _check(load().dh_ctx_read_lb_trace(self._h, _ptr(out), n.value, C.byref(n)))
         return out

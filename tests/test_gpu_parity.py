@@ -473,8 +473,8 @@ def test_fused_equals_split_bitwise(dh, seed, P, M, n_T, N):
         res[path] = (pr, sse, bad, lp)
     s, f = res[_native.PATH_SPLIT], res[_native.PATH_FUSED]
     assert np.array_equal(surf.price(rec, N), f[0])
-    # auto: fused for requests of <= 1,024 tables whose groups are single tiles
-    assert ctx.last_path == (_native.PATH_FUSED if P * len(set(T)) <= 1024 else _native.PATH_SPLIT)
+    # auto: fused wherever every group is one tile (these are no generator-sized small-tile calls)
+    assert ctx.last_path == _native.PATH_FUSED
     for a, b in zip(s, f):
         assert np.array_equal(a, b), np.max(np.abs(np.asarray(a, float) - np.asarray(b, float)))
     assert np.array_equal(f[0], f[3])

@@ -23,9 +23,12 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--driver", default="scipy", choices=["scipy", "device"])
     ap.add_argument("--starts", type=int, default=3)
+    ap.add_argument("--path", type=int, default=0, help="0 auto, 1 split, 2 fused")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     opts, S0, r = bench.make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
+    from dhcos import _native
+    _native.default_context().set_path(args.path)
     for _ in range(2):                      # warm-up (surface upload, JIT of nothing, caches)
         np.random.seed(0)
         DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"]).calibrate(300, args.starts, driver=args.driver)
