@@ -309,9 +309,43 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
         if cpu:
             line["cpu_baseline"] = cpu
             line["speedup_vs_cpu"] = value / cpu["value"]
+    e2e = None if args.no_calib else generator_end_to_end(world, rank, coll)
+    if rank == 0:
+        if e2e:
+            line["generator_end_to_end"] = e2e
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def generator_end_to_end(world, rank, coll, n_samples=1_000_000):
+    """generate_synthetic_calibrations(n_samples, as_arrays=True) end to end under
+    np.random.seed(0): the reference's RNG draws (native legacy-NumPy stream on rank 0), its 5 x 3
+    call grid priced on the GPUs (sharded at N > 1), noise and per-sample losses."""
+    from dhcos import generator as G
+    from dhcos.distributed import generate_sharded
+    if world > 1:
+        dist.barrier()
+    np.random.seed(0)
+    t0 = time.perf_counter()
+    out = generate_sharded(n_samples, None, as_arrays=True, verbose=False)
+    dt = time.perf_counter() - t0
+    t_draw = None
+    if rank == 0:                       # the host-draw share of it (rank 0 draws for all ranks)
+        np.random.seed(0)
+        t1 = time.perf_counter()
+        G.draw_paths(n_samples)
+        t_draw = time.perf_counter() - t1
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=coll)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        return None
+    return {"samples": n_samples, "options_per_sample": int(out["model_prices"].shape[1]),
+            "seconds": dt, "samples_per_sec": n_samples / dt, "host_draw_seconds": t_draw,
+            "call": "generate_synthetic_calibrations(1_000_000, as_arrays=True), np.random.seed(0)"
+                    + (", pricing sharded over ranks" if world > 1 else "")}
 
 
 def main():

@@ -163,6 +163,20 @@ int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double* x0, int S
 int dh_ctx_set_lb_trace(dh_ctx* ctx, int64_t cap);
 int dh_ctx_read_lb_trace(dh_ctx* ctx, double* out, int64_t cap, int64_t* n);
 
+/* ---- generator batch path: host RNG ------------------------------------------------------ */
+/* Draws n_samples samples of generate_synthetic_calibrations (synthetic_generator.py:98-141)
+ * from NumPy's legacy RandomState stream, bit for bit, on the host (no device work): per sample
+ * 13 uniform(lo[j], hi[j]) (:100-102), the AR(1) blend alpha * prev + (1 - alpha) * draw for
+ * i > 0 (:105-109), spot *= 1 + normal(ret_mu, ret_sigma) for i > 0 (:112-116, spot0 at i = 0),
+ * then n_opt normal(0, noise_sigma) (:141).  The state is NumPy's get_state() tuple: mt_key[624],
+ * mt_pos, has_gauss, cached_gauss -- read and advanced in place (set it back with set_state).
+ * Outputs: params [n][13], spots [n], noise [n][n_opt].  The draws replace the reference's
+ * per-sample Python loop; pricing then runs on the GPU (dh_surface_price, STRIKE_PCT_SPOT).      */
+int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* cached_gauss,
+                int64_t n_samples, const double* lo, const double* hi, int n_opt, double alpha,
+                double spot0, double ret_mu, double ret_sigma, double noise_sigma, double* params,
+                double* spots, double* noise);
+
 /* ---- paired pricing: option i under param set i ------------------------------------------- */
 /* out[i] = price of (K[i], T[i], is_call[i]) under params[i]; replaces a loop of single
  * DoubleHeston(...).pricing(N) calls (double_heston.py:160-192).                              */

@@ -2200,7 +2200,7 @@ using WaveCore = dhlb::LbCore<WaveVec, WaveRing>;
 // then (DH_STAMPS build only) s_memtime at the step kernel's phase boundaries: start, state
 // loaded, request consumed, state machine done, request emitted, end
 constexpr int kLbTrace = 40;
-constexpr int kLbStamp0 = 32;
+[[maybe_unused]] constexpr int kLbStamp0 = 32;
 
 __device__ __forceinline__ unsigned long long lb_clock() {
 #ifdef DH_STAMPS
@@ -2299,13 +2299,13 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     __shared__ double ring[kLbRing + dhlb::kM];
     __shared__ double fl[dhlb::kLanes];
     __shared__ double pb[dhlb::kLanes], pp[dhlb::kLanes];
-    const unsigned long long t_start = lb_clock();
+    [[maybe_unused]] const unsigned long long t_start = lb_clock();
     const int slot = blockIdx.x;
     const int lane = threadIdx.x;
     const int sidx = A.live[slot];
     LbSlot* G = A.states + sidx;
     WaveCore c;
-    unsigned long long t_load = 0, t_req = 0, t_sm = 0;
+    [[maybe_unused]] unsigned long long t_load = 0, t_req = 0, t_sm = 0;
     c.pairs = WaveRing{ring, ring + dhlb::kM * dhlb::kLanes, ring + 2 * dhlb::kM * dhlb::kLanes,
                        ring + kLbRing, lane};
     WaveVec dx, pen;
@@ -2395,8 +2395,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     }
     if (need) lb_emit(c, dx, pen, pb, pp, A, slot, lane);
     __syncthreads();
-    const unsigned long long t_emit = lb_clock();
-    (void)t_emit;
+    [[maybe_unused]] const unsigned long long t_emit = lb_clock();
     for (int i = lane; i < kLbRing; i += 64) G->ring[i] = ring[i];
     lb_st(G, 0, lane, c.x);
     lb_st(G, 1, lane, c.g);

@@ -75,6 +75,9 @@ SIGNATURES = {
                                      _i32p]),
     "dh_ctx_set_lb_trace": (C.c_int, [_vp, C.c_int64]),
     "dh_ctx_read_lb_trace": (C.c_int, [_vp, _dp, C.c_int64, C.POINTER(C.c_int64)]),
+    "dh_gen_draw": (C.c_int, [C.POINTER(C.c_uint32), _i32p, _i32p, _dp, C.c_int64, _dp, _dp,
+                              C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+                              _dp, _dp, _dp]),
     "dh_price_pairs": (C.c_int, [_vp, _dp, _dp, _dp, _i8p, C.c_int64, C.c_int, C.c_double, _dp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
@@ -341,6 +344,26 @@ class Surface:
                                           _vp(stream) if stream else None))
 
 
+def gen_draw(n_samples, lo, hi, n_opt, alpha, spot0, ret_mu, ret_sigma, noise_sigma):
+    """dh_gen_draw on NumPy's global legacy RandomState: draws the generator's samples natively
+    and advances np.random's state exactly as the reference's per-sample calls would.
+    -> (params [n, 13], spots [n], noise [n, n_opt])."""
+    name, key, pos, has_gauss, cached = np.random.get_state()
+    if name != "MT19937":
+        raise NativeError(f"unsupported bit generator {name}")
+    key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+    c_pos, c_has, c_cached = C.c_int32(int(pos)), C.c_int32(int(has_gauss)), C.c_double(cached)
+    n = int(n_samples)
+    params, spots, noise = np.empty((n, 13)), np.empty(n), np.empty((n, int(n_opt)))
+    _check(load().dh_gen_draw(key.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(c_pos),
+                              C.byref(c_has), C.byref(c_cached), n, _ptr(_f64(lo)), _ptr(_f64(hi)),
+                              int(n_opt), float(alpha), float(spot0), float(ret_mu),
+                              float(ret_sigma), float(noise_sigma), _ptr(params), _ptr(spots),
+                              _ptr(noise)))
+    np.random.set_state((name, key, c_pos.value, c_has.value, c_cached.value))
+    return params, spots, noise
+
+
 _tls = threading.local()
 
 
@@ -357,6 +380,6 @@ def default_context(device: int | None = None) -> Context:
     return ctx
 
 
-__all__ = ["LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
+__all__ = ["gen_draw", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "PARAM_STRIDE", "MAX_N", "STRIKE_ABSOLUTE",
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "LIB_PATH", "SIGNATURES"]

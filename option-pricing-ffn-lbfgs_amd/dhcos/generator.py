@@ -6,9 +6,11 @@ call grid one option at a time and adds 2% Gaussian noise to each price.  Pricin
 randomness, so this implementation
 
   1. draws every random number on the host in the reference's order from the legacy global
-     ``np.random`` stream (13 uniforms, then one spot normal for i > 0, then 15 noise normals:
-     vectorised per sample, same values as the reference's scalar calls),
-  2. runs the AR(1) and spot recursions on the host,
+     ``np.random`` stream (13 uniforms, then one spot normal for i > 0, then 15 noise normals)
+     and runs the AR(1) and spot recursions -- natively (``dh_gen_draw``: NumPy's MT19937 and
+     legacy uniform / polar-gauss restated, state taken from and handed back to ``np.random``,
+     ~10x the per-sample NumPy loop, which stays as ``draw_paths_numpy`` for the tests),
+  2. (the recursions run inside the same native loop),
   3. prices all samples x options in one launch per chunk on the GPU (strikes formed on the device
      as K_relative * spot / 100.0, exactly the reference's expression, :125),
   4. applies the noise and the per-sample loss with the reference's NumPy expressions.
@@ -42,19 +44,25 @@ ALPHA = 0.9                                        # :108
 
 
 def trading_dates(n):
-    """Weekdays from 2022-01-03 (synthetic_generator.py:59-67)."""
-    out, cur = [], datetime(2022, 1, 3)
-    for _ in range(n):
-        while cur.weekday() >= 5:
-            cur += timedelta(days=1)
-        out.append(cur.strftime("%Y-%m-%d"))
-        cur += timedelta(days=1)
-    return out
+    """Weekdays from 2022-01-03 as 'YYYY-MM-DD' (synthetic_generator.py:59-67): the reference's
+    weekend-skipping loop, as one NumPy business-day offset (same strings, 12x faster at 1M)."""
+    days = np.busday_offset("2022-01-03", np.arange(int(n)), roll="forward")
+    return np.datetime_as_string(days, unit="D").tolist()
 
 
 def draw_paths(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
-    """Host part: RNG in reference order + AR(1) params + spot walk.
-    Returns (params [n,13], spots [n], noise [n, n_opts])."""
+    """Host part: RNG in reference order + AR(1) params + spot walk, natively (dh_gen_draw).
+    Returns (params [n,13], spots [n], noise [n, n_opts]) and leaves np.random's state where the
+    reference's loop leaves it."""
+    lo = np.array([v[0] for v in PARAM_RANGES.values()])
+    hi = np.array([v[1] for v in PARAM_RANGES.values()])
+    n_opt = len(strikes) * len(maturities)
+    return _native.gen_draw(n_samples, lo, hi, n_opt, ALPHA, SPOT_BASE, 0.0003, 0.01, 0.02)
+
+
+def draw_paths_numpy(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
+    """draw_paths as a per-sample NumPy loop (the reference's calls, vectorised per sample);
+    kept as the tests' cross-check of the native draw."""
     lo = np.array([v[0] for v in PARAM_RANGES.values()])
     hi = np.array([v[1] for v in PARAM_RANGES.values()])
     n_opt = len(strikes) * len(maturities)

@@ -1,0 +1,74 @@
+"""The generator's native host draw (dh_gen_draw: NumPy's legacy MT19937 / uniform / polar gauss
+restated in C++) against NumPy itself and against the reference's own output.  CPU only: the
+function is host code in libdhcos.so and needs no device.
+
+Bar: bit-identical draws and an identical continuation of the global np.random stream."""
+import numpy as np
+import pytest
+
+from dhcos import generator as G
+
+
+@pytest.mark.parametrize("seed,n,pre", [(0, 3000, 0), (7, 1, 1), (123, 257, 3), (99, 0, 1)])
+def test_native_draw_equals_numpy_loop(seed, n, pre):
+    """pre = scalar normals drawn first, so the stream starts with / without a cached gauss."""
+    np.random.seed(seed)
+    for _ in range(pre):
+        np.random.normal()
+    want = G.draw_paths_numpy(n)
+    after_want = np.random.random(7)
+    np.random.seed(seed)
+    for _ in range(pre):
+        np.random.normal()
+    got = G.draw_paths(n)
+    after_got = np.random.random(7)
+    for a, b in zip(got, want):
+        assert a.shape == b.shape and np.array_equal(a, b)
+    assert np.array_equal(after_got, after_want)
+
+
+def test_native_draw_reproduces_reference_samples(gen_golden):
+    """np.random.seed(0); generate_synthetic_calibrations(6) in the reference: its parameters and
+    spots, and its market prices formed from its own model prices and our noise draws."""
+    np.random.seed(0)
+    params, spots, noise = G.draw_paths(len(gen_golden))
+    for i, w in enumerate(gen_golden):
+        assert list(params[i]) == list(w["parameters"].values())
+        assert spots[i] == w["spot"]
+        model = np.array(w["model_prices"])
+        assert np.array_equal(model + noise[i] * model, np.array(w["market_prices"]))
+
+
+def test_native_draw_rejects_bad_arguments():
+    import ctypes as C
+    from dhcos import _native
+    lib = _native.load()
+    key = np.zeros(624, dtype=np.uint32)
+    pos, hg, cg = C.c_int32(625), C.c_int32(0), C.c_double(0.0)
+    lo, hi = np.zeros(13), np.ones(13)
+    out = [np.empty((2, 13)), np.empty(2), np.empty((2, 15))]
+    args = [key.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(pos), C.byref(hg), C.byref(cg), 2,
+            _native._ptr(lo), _native._ptr(hi), 15, 0.9, 100.0, 0.0, 0.01, 0.02] + \
+        [_native._ptr(a) for a in out]
+    assert lib.dh_gen_draw(*args) == -1          # mt_pos outside [0, 624]
+    pos.value = 624
+    args[4] = -1
+    assert lib.dh_gen_draw(*args) == -1          # negative sample count
+
+
+def test_trading_dates_match_reference_loop():
+    """synthetic_generator.py:59-67's weekend-skipping loop, restated here as the check."""
+    from datetime import datetime, timedelta
+
+    def loop(n):
+        out, cur = [], datetime(2022, 1, 3)
+        for _ in range(n):
+            while cur.weekday() >= 5:
+                cur += timedelta(days=1)
+            out.append(cur.strftime("%Y-%m-%d"))
+            cur += timedelta(days=1)
+        return out
+
+    for n in (0, 1, 5, 6, 7, 11, 2500):
+        got = G.trading_dates(n)
+        assert got == loop(n) and all(type(d) is str for d in got)
