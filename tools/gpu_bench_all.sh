@@ -2,8 +2,8 @@
 # Full bench lines (CPU baseline included) for every config -> gpurun_out/bench_<cfg>.json
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
-for c in ${CONFIGS:-c2 c1 c3 c5}; do
-  if [ $c = c5 ]; then ST="--steps 5 --warmup 1"; else ST=""; fi
+for c in ${CONFIGS:-c2 c1 c3 c4 c5}; do
+  if [ $c = c5 ]; then ST="--steps 5 --warmup 1"; elif [ $c = c4 ]; then ST="--steps 50 --warmup 5"; else ST=""; fi
   timeout -k 10 400 python bench.py --config $c $ST > gpurun_out/bench_$c.log 2>&1 || { echo "bench $c failed"; tail -5 gpurun_out/bench_$c.log; exit 1; }
   tail -1 gpurun_out/bench_$c.log > gpurun_out/bench_$c.json
   python - gpurun_out/bench_$c.json $c <<'PY'

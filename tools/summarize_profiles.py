@@ -50,10 +50,11 @@ def main():
     tpath = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     md = [f"# Profile summary {args.tag}", "",
-          "One request = cos_fused_kernel (requests of <= 1,024 tables), or cos_table_kernel + the "
-          "option kernel (cos_option_kernel, or cos_option_small_kernel for large calls on "
-          "<=16-option tiles). Durations: rocprofv3 --kernel-trace --stats average; counters: "
-          "per-launch medians of separate --pmc passes.", ""]
+          "One request = cos_fused_kernel (every maturity group one tile: C1-C4), or "
+          "cos_table_kernel + the option kernel (cos_option_kernel for multi-tile groups, "
+          "cos_option_small_kernel for large calls on <=16-option tiles: C5). Durations: "
+          "rocprofv3 --kernel-trace --stats average; counters: per-launch medians of separate "
+          "--pmc passes.", ""]
     for c in args.configs.split(","):
         stats = os.path.join(args.src, f"{args.tag}_{c}_stats_kernel_stats.csv")
         if not os.path.exists(stats):
