@@ -163,6 +163,21 @@ int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double* x0, int S
 int dh_ctx_set_lb_trace(dh_ctx* ctx, int64_t cap);
 int dh_ctx_read_lb_trace(dh_ctx* ctx, double* out, int64_t cap, int64_t* n);
 
+/* ---- one-shot forms (SURVEY.md 8(b)'s proposed exports; a surface is built per call) ------- */
+/* out[p*M + m] = price of option m (K, T, is_call) under params[p] (13 model params, S0, r, q):
+ * dh_surface_create + dh_surface_price + dh_surface_destroy.  Replaces P x M calls of
+ * DoubleHeston(...).pricing(N) (double_heston.py:160-192).                                      */
+int dh_price_batch(dh_ctx* ctx, const double* params, int64_t P, const double* K, const double* T,
+                   const int8_t* is_call, int M, int N, double L, double* out);
+/* compute_loss (lbfgs_calibrator.py:118-177) of S unconstrained points x[S][13], all on the
+ * device: transform (exp / tanh / identity, :62-87), Feller penalty (:113-116), the surface's
+ * loss terms, then loss[s] = n_invalid[s] ? 1e10 : sse / M + penalty (:152-166).  M == 0 gives
+ * NaN (np.mean([]), :163); a zero market price gives inf.  One FD request = the 14 points
+ * x, x + h_i e_i.                                                                               */
+int dh_loss_batch(dh_ctx* ctx, const double* x, int S, const double* K, const double* T,
+                  const int8_t* is_call, const double* mkt, int M, double S0, double r, int N,
+                  double L, double* loss, int32_t* n_invalid);
+
 /* ---- generator batch path: host RNG ------------------------------------------------------ */
 /* Draws n_samples samples of generate_synthetic_calibrations (synthetic_generator.py:98-141)
  * from NumPy's legacy RandomState stream, bit for bit, on the host (no device work): per sample

@@ -2605,3 +2605,106 @@ extern "C" int dh_ctx_read_lb_trace(dh_ctx* ctx, double* out, int64_t cap, int64
     *n = (int64_t)cnt;
     return DH_OK;
 }
+
+// ----------------------------------------------------------------------------------------------
+// one-shot entry points in the shape SURVEY.md 8(b) proposes (a surface per call)
+// ----------------------------------------------------------------------------------------------
+namespace {
+
+// unconstrained x [S][13] -> param records (exp / tanh / identity, lbfgs_calibrator.py:62-87)
+// and Feller penalties (:113-116); one thread per set, the expressions of lb_emit
+__global__ void x_records_kernel(const double* __restrict__ x, int S, double S0, double r,
+                                 double* __restrict__ rec, double* __restrict__ pen) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    double p[dhlb::kN];
+#pragma unroll
+    for (int i = 0; i < dhlb::kN; ++i) p[i] = lb_transform(i, x[(size_t)s * dhlb::kN + i]);
+    const double v1 = p[3] * p[3] - 2.0 * p[1] * p[2];
+    const double v2 = p[8] * p[8] - 2.0 * p[6] * p[7];
+    pen[s] = 1000.0 * ((v1 > 0.0 ? v1 : 0.0) + (v2 > 0.0 ? v2 : 0.0));
+    double* out = rec + (size_t)s * DH_PARAM_STRIDE;
+#pragma unroll
+    for (int i = 0; i < dhlb::kN; ++i) out[i] = p[i];
+    out[13] = S0;
+    out[14] = r;
+    out[15] = 0.0;
+}
+
+// loss = n_bad ? 1e10 : sse / M + penalty (lbfgs_calibrator.py:152-166)
+__global__ void loss_finalize_kernel(const double* __restrict__ sse, const int* __restrict__ bad,
+                                     const double* __restrict__ pen, int S, int M,
+                                     double* __restrict__ loss) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    loss[s] = bad[s] > 0 ? kInvalidLoss : sse[s] / (double)M + pen[s];
+}
+
+}  // namespace
+
+extern "C" int dh_price_batch(dh_ctx* ctx, const double* params, int64_t P, const double* K,
+                              const double* T, const int8_t* is_call, int M, int N, double L,
+                              double* out) {
+    if (!ctx || (P > 0 && M > 0 && (!params || !out))) return fail(DH_E_ARG, "null argument");
+    if (P < 0) return fail(DH_E_ARG, "P < 0");
+    dh_surface* s = nullptr;
+    int rc = dh_surface_create(ctx, K, T, is_call, nullptr, M, DH_STRIKE_ABSOLUTE, &s);
+    if (rc) return rc;
+    rc = dh_surface_price(ctx, s, params, P, N, L, out);
+    dh_surface_destroy(s);
+    return rc;
+}
+
+extern "C" int dh_loss_batch(dh_ctx* ctx, const double* x, int S, const double* K, const double* T,
+                             const int8_t* is_call, const double* mkt, int M, double S0, double r,
+                             int N, double L, double* loss, int32_t* n_invalid) {
+    if (!ctx || (S > 0 && (!x || !loss || !n_invalid))) return fail(DH_E_ARG, "null argument");
+    if (S < 0) return fail(DH_E_ARG, "S < 0");
+    if (M > 0 && !mkt) return fail(DH_E_ARG, "mkt is null");
+    int rc = check_N(N);
+    if (rc) return rc;
+    if (S == 0) return DH_OK;
+    if (M == 0) {                                   // np.mean([]) -> nan (lbfgs_calibrator.py:163)
+        for (int i = 0; i < S; ++i) {
+            loss[i] = __builtin_nan("");
+            n_invalid[i] = 0;
+        }
+        return DH_OK;
+    }
+    rc = set_device(ctx);
+    if (rc) return rc;
+    dh_surface* s = nullptr;
+    rc = dh_surface_create(ctx, K, T, is_call, mkt, M, DH_STRIKE_ABSOLUTE, &s);
+    if (rc) return rc;
+    hipStream_t st = ctx->stream;
+    const size_t xb = (size_t)S * dhlb::kN * 8;
+    auto run = [&]() -> int {
+        HIP_TRY(ctx->aux0.reserve(xb));
+        HIP_TRY(ctx->aux1.reserve((size_t)S * DH_PARAM_STRIDE * 8));
+        HIP_TRY(ctx->aux2.reserve((size_t)S * 8 * 3));     // pen | sse | loss
+        HIP_TRY(ctx->aux3.reserve((size_t)S * 4));
+        double* d_x = (double*)ctx->aux0.ptr;
+        double* d_rec = (double*)ctx->aux1.ptr;
+        double* d_pen = (double*)ctx->aux2.ptr;
+        double* d_sse = d_pen + S;
+        double* d_loss = d_sse + S;
+        int* d_bad = (int*)ctx->aux3.ptr;
+        HIP_TRY(hipMemcpyAsync(d_x, x, xb, hipMemcpyHostToDevice, st));
+        const unsigned b = (unsigned)((S + 255) / 256);
+        hipLaunchKernelGGL(x_records_kernel, dim3(b), dim3(256), 0, st, d_x, S, S0, r, d_rec, d_pen);
+        HIP_TRY(hipGetLastError());
+        int e = surface_loss_launch(ctx, s, d_rec, S, N, L, d_sse, (int32_t*)d_bad, nullptr, st,
+                                    nullptr);
+        if (e) return e;
+        hipLaunchKernelGGL(loss_finalize_kernel, dim3(b), dim3(256), 0, st, d_sse, d_bad, d_pen, S,
+                           s->M, d_loss);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(loss, d_loss, (size_t)S * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(n_invalid, d_bad, (size_t)S * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return DH_OK;
+    };
+    rc = run();
+    dh_surface_destroy(s);
+    return rc;
+}

@@ -78,6 +78,10 @@ SIGNATURES = {
     "dh_gen_draw": (C.c_int, [C.POINTER(C.c_uint32), _i32p, _i32p, _dp, C.c_int64, _dp, _dp,
                               C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                               _dp, _dp, _dp]),
+    "dh_price_batch": (C.c_int, [_vp, _dp, C.c_int64, _dp, _dp, _i8p, C.c_int, C.c_int,
+                                 C.c_double, _dp]),
+    "dh_loss_batch": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp, _i8p, _dp, C.c_int, C.c_double,
+                                C.c_double, C.c_int, C.c_double, _dp, _i32p]),
     "dh_price_pairs": (C.c_int, [_vp, _dp, _dp, _dp, _i8p, C.c_int64, C.c_int, C.c_double, _dp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
@@ -229,6 +233,34 @@ class Context:
             _check(load().dh_price_pairs(self._h, _ptr(params), _ptr(K), _ptr(T), _ptr(ic, _i8p),
                                          P, int(N), float(L), _ptr(out)))
         return out
+
+    def price_batch(self, params, K, T, is_call, N=128, L=10.0):
+        """dh_price_batch: out [P, M] for every (param set, option); a surface per call."""
+        params = _f64(params).reshape(-1, PARAM_STRIDE)
+        P = params.shape[0]
+        K, T = _f64(K).reshape(-1), _f64(T).reshape(-1)
+        M = K.size
+        ic = np.ascontiguousarray(is_call, dtype=np.int8).reshape(M)
+        out = np.empty((P, M))
+        with self._lock:
+            _check(load().dh_price_batch(self._h, _ptr(params), P, _ptr(K), _ptr(T),
+                                         _ptr(ic, _i8p), M, int(N), float(L), _ptr(out)))
+        return out
+
+    def loss_batch(self, X, K, T, is_call, mkt, S0, r, N=128, L=10.0):
+        """dh_loss_batch: compute_loss of every row of unconstrained X [S, 13] over the market
+        (K, T, is_call, mkt) -> (loss [S], n_invalid [S]); a surface per call."""
+        X = _f64(X).reshape(-1, 13)
+        S = X.shape[0]
+        K, T, mkt = _f64(K).reshape(-1), _f64(T).reshape(-1), _f64(mkt).reshape(-1)
+        M = K.size
+        ic = np.ascontiguousarray(is_call, dtype=np.int8).reshape(M)
+        loss, bad = np.empty(S), np.empty(S, dtype=np.int32)
+        with self._lock:
+            _check(load().dh_loss_batch(self._h, _ptr(X), S, _ptr(K), _ptr(T), _ptr(ic, _i8p),
+                                        _ptr(mkt), M, float(S0), float(r), int(N), float(L),
+                                        _ptr(loss), _ptr(bad, _i32p)))
+        return loss, bad
 
     def cf(self, params16, u, tau):
         p = _f64(params16).reshape(PARAM_STRIDE)

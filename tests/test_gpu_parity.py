@@ -519,3 +519,33 @@ def test_fused_loss_handoff_back_to_back(dh):
             assert np.array_equal(sse, got_sse[i]) and np.array_equal(bad, got_bad[i]), i
     finally:
         ctx.set_path(0)
+
+
+def test_one_shot_price_and_loss_batch(dh, calib_golden):
+    """dh_price_batch / dh_loss_batch (SURVEY 8(b)'s proposed exports, a surface per call) equal
+    the surface path bit for bit (prices), and the calibrator's compute_loss within the loss
+    tolerance (the transforms run on the device here, in NumPy there); edge semantics: NaN for
+    an empty market, inf for a zero market price."""
+    from dhcos import _native
+    from dhcos.calibrator import fd_request_points
+    ctx = _native.default_context()
+    params, rec, K, T, call = _surface_case(51, P=5, M=300, n_T=6, N=128)
+    surf = _native.Surface(ctx, K, T, call)
+    assert np.array_equal(ctx.price_batch(rec, K, T, call, 128), surf.price(rec, 128))
+    mkt = calib_golden["test_market"]
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, mkt)
+    X, _ = fd_request_points(cal.get_initial_guess(0))
+    Km = [o["strike"] for o in mkt]
+    Tm = [o["maturity"] for o in mkt]
+    cm = [1] * len(mkt)
+    pm = [o["price"] for o in mkt]
+    loss, bad = ctx.loss_batch(X, Km, Tm, cm, pm, 100.0, 0.05, 128)
+    want = cal.loss_batch(X, track=False)
+    assert (bad == 0).all() and rel_close(loss, want, LOSS_RTOL, 0).all(), np.max(np.abs(loss / want - 1))
+    assert rel_close(loss[0], calib_golden["loss_at_guesses"][0], LOSS_RTOL, 0)
+    l0, b0 = ctx.loss_batch(X[:2], [], [], [], [], 100.0, 0.05, 128)
+    assert np.isnan(l0).all() and (b0 == 0).all()
+    pz = list(pm)
+    pz[3] = 0.0
+    lz, _ = ctx.loss_batch(X[:1], Km, Tm, cm, pz, 100.0, 0.05, 128)
+    assert np.isinf(lz[0])
