@@ -2434,8 +2434,8 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
     int rc = check_N(N);
     if (rc) return rc;
     if (S < 0) return fail(DH_E_ARG, "S < 0");
-    if (opt->maxiter < 1 || opt->maxfun < 1 || opt->maxls < 1)
-        return fail(DH_E_ARG, "maxiter, maxfun and maxls must be >= 1");
+    if (opt->maxiter < 0 || opt->maxfun < 0 || opt->maxls < 1)   // SciPy: maxls must be > 0
+        return fail(DH_E_ARG, "maxiter and maxfun must be >= 0, maxls >= 1");
     if (n_launches) *n_launches = 0;
     if (S == 0) return DH_OK;
     rc = set_device(ctx);

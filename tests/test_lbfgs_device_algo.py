@@ -15,7 +15,6 @@ messages and the solution to a tolerance.  The tolerances below are stated per c
     ABNORMAL after 20 line-search trials): bit-identical x and fun, nit 0, nfev 21.
 CPU only."""
 import ctypes as C
-import json
 import os
 
 import numpy as np
@@ -100,6 +99,8 @@ def _kinked_fd(x):
     ("kink-fd", _kinked_fd, np.array([0.8, 0.9] + [0.3] * (N_PARAMS - 2)), 300, _MAXFUN, 1e-12),
     ("maxiter", _rosen, np.full(N_PARAMS, 3.0), 5, _MAXFUN, 1e-12),
     ("maxfun", _rosen, np.full(N_PARAMS, -2.0), 300, 7, 1e-12),
+    ("maxiter-0", _quad, np.zeros(N_PARAMS), 0, _MAXFUN, 1e-12),
+    ("maxfun-0", _quad, np.zeros(N_PARAMS), 300, 0, 1e-12),
 ])
 def test_state_machine_matches_scipy(lbhost, name, fun, x0, maxiter, maxfun, xtol):
     want = minimize(fun=fun, x0=x0, method="L-BFGS-B", jac=True,
