@@ -361,6 +361,7 @@ struct FactorC {
 
 __device__ __forceinline__ FactorC factor_consts(double v0, double kap, double th, double sig,
                                                  double rho) {
+#pragma clang fp contract(off)   // the same bits in every prologue form (table, fused)
     FactorC F;
     F.kap = kap;
     F.rs = rho * sig;
@@ -412,6 +413,7 @@ struct CfConsts {
 };
 
 __device__ __forceinline__ CfConsts cf_consts(const Params& P, double tau) {
+#pragma clang fp contract(off)   // the same bits in every prologue form (table, fused)
     CfConsts C;
     C.f1 = factor_consts(P.v01, P.k1, P.t1, P.s1, P.r1);
     C.f2 = factor_consts(P.v02, P.k2, P.t2, P.s2, P.r2);
@@ -463,6 +465,7 @@ __device__ __forceinline__ void load_sincos_table(double2* sct) {
 __device__ __forceinline__ void factor_cumulants(double tau, double r, double v0, double lm,
                                                  double vb, double vv, double rho, double& c1,
                                                  double& c2) {
+#pragma clang fp contract(off)   // the same bits in every prologue form (table, fused)
     const double ek = exp(-lm * tau);
     c1 = r * tau + (1.0 - ek) * (vb - v0) / (2.0 * lm) - vb * tau / 2.0;
     const double lm2 = lm * lm, lm3 = lm2 * lm, vv2 = vv * vv;   // np.power(lm, 3) ~ lm*lm*lm
@@ -477,6 +480,7 @@ __device__ __forceinline__ void factor_cumulants(double tau, double r, double v0
 // Un-clamped truncation range c1 -/+ L sqrt|c2| (double_heston.py:120-132).
 __device__ __forceinline__ void trunc_unclamped(const Params& P, double T, double L, double& a,
                                                 double& b) {
+#pragma clang fp contract(off)
     double c1a, c2a, c1b, c2b;
     factor_cumulants(T, P.r, P.v01, P.k1, P.t1, P.s1, P.r1, c1a, c2a);
     factor_cumulants(T, P.r, P.v02, P.k2, P.t2, P.s2, P.r2, c1b, c2b);

@@ -171,6 +171,7 @@ static_assert(sizeof(dh::CfConsts) == 16 * sizeof(double), "CfConsts layout");
 // Prologue of table q = (p, g) of a launch: truncation range, CF constants and the staged values
 // above, written to c[0 .. kTabC).
 __device__ __forceinline__ void table_prologue(const PriceArgs& A, int64_t q, double* c) {
+#pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
     const int tpp = tabs_per_p(A);
     const int64_t p = A.p0 + q / tpp;
     const int g = (int)(q % tpp);
@@ -198,6 +199,75 @@ __device__ __forceinline__ void table_prologue(const PriceArgs& A, int64_t q, do
     c[26] = exp(b - 0.1) * (1.0 - kClampMargin);
     c[27] = gr.x;
     c[28] = gr.y;
+}
+
+// table_prologue run by one wave in lockstep (the fused kernel's wave 0): the two variance
+// factors' cumulants and CF constants on alternate lanes, the five exponentials (e^b, e^a, the
+// clamp bounds' e^(a+0.1) and e^(b-0.1), and the jump compensator's e^(mu + sj^2/2)) one per lane,
+// broadcast with readlane.  Every value is the same expression on the same inputs as in
+// table_prologue and cf_consts, so the staged constants are the same bits.
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, int64_t q, double* c,
+                                                    int lane) {
+#pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
+    const int tpp = tabs_per_p(A);
+    const int64_t p = A.p0 + q / tpp;
+    const int g = (int)(q % tpp);
+    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
+    const double T = A.paired ? A.T[p] : A.group_T[g];
+    int2 gr = make_int2((int)p, 1);
+    if (!A.paired) gr = A.groups[g];
+    const bool two = lane & 1;                     // factor 2 on odd lanes
+    const double v0 = two ? P.v02 : P.v01, k = two ? P.k2 : P.k1, th = two ? P.t2 : P.t1;
+    const double sg = two ? P.s2 : P.s1, rh = two ? P.r2 : P.r1;
+    double c1j, c2j;
+    dh::factor_cumulants(T, P.r, v0, k, th, sg, rh, c1j, c2j);   // double_heston.py:101-118
+    const dh::FactorC Fj = dh::factor_consts(v0, k, th, sg, rh);
+    const double c1 = lane_bcast(c1j, 0) + lane_bcast(c1j, 1) + P.lam * T * P.muj;
+    const double c2 = lane_bcast(c2j, 0) + lane_bcast(c2j, 1) +
+                      P.lam * T * (P.sj * P.sj + P.muj * P.muj);
+    const double h = A.L * sqrt(fabs(c2));
+    const double a = c1 - h, b = c1 + h;           // trunc_unclamped (double_heston.py:120-132)
+    const int e_lane = lane < 5 ? lane : 0;
+    const double arg = e_lane == 0 ? b : e_lane == 1 ? a : e_lane == 2 ? a + 0.1
+                     : e_lane == 3 ? b - 0.1 : P.muj + 0.5 * (P.sj * P.sj);
+    const double e = exp(arg);
+    dh::CfConsts CC;
+    double* f1 = (double*)&CC.f1;
+    double* f2 = (double*)&CC.f2;
+    const double* fj = (const double*)&Fj;
+    for (int i = 0; i < (int)(sizeof(dh::FactorC) / 8); ++i) {
+        f1[i] = lane_bcast(fj[i], 0);
+        f2[i] = lane_bcast(fj[i], 1);
+    }
+    const double comp = lane_bcast(e, 4) - 1.0;    // cf_consts
+    CC.drift = (P.r - P.q - P.lam * comp) * T;
+    CC.half_sj2 = 0.5 * (P.sj * P.sj);
+    CC.muj = P.muj;
+    CC.lt = P.lam * T;
+    if (lane == 0) {
+        c[0] = a;
+        c[1] = b;
+        c[2] = e;
+        c[3] = lane_bcast(e, 1);
+        c[4] = 2.0 / (b - a);
+        c[5] = dh::kPi / (b - a);
+        const double* cc = (const double*)&CC;
+        for (int i = 0; i < 16; ++i) c[6 + i] = cc[i];
+        c[22] = P.S0;
+        c[23] = P.r;
+        c[24] = T;
+        c[25] = lane_bcast(e, 2) * (1.0 + kClampMargin);
+        c[26] = lane_bcast(e, 3) * (1.0 - kClampMargin);
+        c[27] = gr.x;
+        c[28] = gr.y;
+    }
 }
 
 #ifndef DH_TABLE_WAVES
@@ -1008,8 +1078,9 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(Price
     const double S0 = prm[13];
     DH_STAMP(A, 0);
 
-    // ---- prologue (thread 0) || per-option staging (wave 0 takes the last indices) ----
-    if (t == 0) table_prologue(A, q, shc);
+    // ---- prologue (wave 0, lane-parallel) || per-option staging (wave 0 takes the last
+    //      indices) ----
+    if (wv == 0) table_prologue_wave(A, q, shc, lane);
     DH_STAMP(A, 8);
     dh::load_sincos_table(sct);
     for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
