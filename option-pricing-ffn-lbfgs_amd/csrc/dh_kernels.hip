@@ -276,6 +276,9 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, int64_t 
 #ifndef DH_OPTION_WAVES
 #define DH_OPTION_WAVES 1
 #endif
+#ifndef DH_FUSED_WAVES
+#define DH_FUSED_WAVES 2
+#endif
 
 // CF entries of one table slot (thread t of TPT): k = t, t + TPT, ..., emitted in increasing k
 // (the k-sums' order) as emit(k, u_k, w_k).
@@ -1046,7 +1049,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
 // cos_option_kernel<tpt2>, so the two paths give the same bits.
 // ----------------------------------------------------------------------------------------------
 template <int TPT1>
-__global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_fused_kernel(PriceArgs A, int tpt2) {
+__global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(PriceArgs A, int tpt2) {
     if (halted(A)) return;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ double shc[kTabC];
