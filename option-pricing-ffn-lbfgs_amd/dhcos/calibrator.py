@@ -253,8 +253,21 @@ class DoubleHestonJumpCalibrator:
         rec[0, 13:] = (self.spot, self.risk_free_rate, 0.0)
         return surf.price(rec, self.N)[0]
 
+    def start_points(self, multi_start: int, x0=None):
+        """The starts calibrate() runs: get_initial_guess(s % 3) in start order (the only
+        consumer of the global RNG, lbfgs_calibrator.py:256).  x0 -- the warm-start hook the
+        reference's docs describe for an FFN prediction (docs/METHODOLOGY.md:112-134, no code
+        there) -- replaces start 0's literature guess: a dict of the 13 model parameters, or an
+        unconstrained 13-vector.  Start 0 draws no random numbers, so the other starts are
+        unchanged."""
+        x0s = [self.get_initial_guess(guess_type=s % 3) for s in range(multi_start)]
+        if x0 is not None and multi_start > 0:
+            x0s[0] = (self.inverse_transform_params(x0) if isinstance(x0, dict)
+                      else np.asarray(x0, dtype=np.float64).reshape(N_PARAMS).copy())
+        return x0s
+
     def calibrate(self, maxiter: int = 300, multi_start: int = 3, *, lockstep: bool = True,
-                  x0s=None, driver: str = "scipy") -> CalibrationResult:
+                  x0s=None, x0=None, driver: str = "scipy") -> CalibrationResult:
         """Multi-start L-BFGS-B; returns the best start (strict ``<`` in start order).
 
         driver="scipy": SciPy's own setulb on the host, one launch per lockstep request (the
@@ -265,7 +278,7 @@ class DoubleHestonJumpCalibrator:
         start_time = time.time()
         # draw every start's x0 in start order (the only consumer of the global RNG, :256)
         if x0s is None:
-            x0s = [self.get_initial_guess(guess_type=s % 3) for s in range(multi_start)]
+            x0s = self.start_points(multi_start, x0)
         if driver == "device":
             outcomes = run_starts_device(self, x0s, maxiter)
         elif driver == "scipy":

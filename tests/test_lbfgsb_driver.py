@@ -86,3 +86,21 @@ def test_run_starts_lockstep_and_sequential_match_minimize(calib_golden):
         want = _minimize_start(cal.loss_and_grad, x, 12)
         _same(lock[s][0], want)
         _same(seq[s][0], want)
+
+
+def test_warm_start_hook_replaces_start_zero_only(calib_golden):
+    """calibrate(x0=...) (the FFN warm-start hook): start 0 becomes the given
+    point (dict of model parameters or unconstrained vector); the random starts are unchanged."""
+    from dhcos.calibrator import DoubleHestonJumpCalibrator
+    cal = DoubleHestonJumpCalibrator(100.0, 0.05, calib_golden["test_market"])
+    np.random.seed(3)
+    plain = cal.start_points(4)
+    prm = cal.transform_params(plain[1] + 0.01)
+    np.random.seed(3)
+    warm = cal.start_points(4, x0=prm)
+    np.testing.assert_allclose(warm[0], plain[1] + 0.01, rtol=0, atol=1e-12)
+    for a, b in zip(warm[1:], plain[1:]):
+        assert np.array_equal(a, b)
+    np.random.seed(3)
+    vec = cal.start_points(4, x0=plain[2])
+    assert np.array_equal(vec[0], plain[2]) and np.array_equal(vec[3], plain[3])
