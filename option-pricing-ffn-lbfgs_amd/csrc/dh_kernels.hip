@@ -1430,6 +1430,7 @@ struct dh_ctx {
     DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, cl_mask,
         cl_price, aux0, aux1, aux2, aux3;
     HostBuf h_params, h_loss;  // zero-copy inputs / outputs of small host-API loss requests
+    HostBuf h_pairs;           // zero-copy inputs / outputs of small dh_price_pairs calls
     DevBuf lb_state, lb_rec, lb_sse, lb_bad, lb_live, lb_done, lb_x0;   // dh_calibrate_lbfgs
     HostBuf h_lb;              // finished flags / live list of dh_calibrate_lbfgs
     DevBuf lb_trace, lb_trace_n;   // diagnostic request trace of dh_calibrate_lbfgs
@@ -1728,6 +1729,7 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     ctx->h_params.release();
     ctx->h_loss.release();
     ctx->h_lb.release();
+    ctx->h_pairs.release();
     for (hipEvent_t e : ctx->lb_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2065,27 +2067,53 @@ int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const dou
     rc = set_device(ctx);
     if (rc) return rc;
     const size_t pb = (size_t)P * DH_PARAM_STRIDE * 8, vb = (size_t)P * 8;
-    HIP_TRY(ctx->params.reserve(pb));
-    HIP_TRY(ctx->out.reserve(vb));
-    HIP_TRY(ctx->aux0.reserve(vb));
-    HIP_TRY(ctx->aux1.reserve(vb));
-    HIP_TRY(ctx->aux2.reserve((size_t)P));
-    HIP_TRY(ctx->aux3.reserve((size_t)P * 4));
-    std::vector<int> ident((size_t)P);
-    std::iota(ident.begin(), ident.end(), 0);
     hipStream_t st = ctx->stream;
-    HIP_TRY(hipMemcpyAsync(ctx->params.ptr, params, pb, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->aux0.ptr, K, vb, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->aux1.ptr, T, vb, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->aux2.ptr, is_call, (size_t)P, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->aux3.ptr, ident.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
     PriceArgs A{};
-    A.prm = (const double*)ctx->params.ptr;
     A.P = P;
-    A.K = (const double*)ctx->aux0.ptr;
-    A.T = (const double*)ctx->aux1.ptr;
-    A.call = (const int8_t*)ctx->aux2.ptr;
-    A.perm = (const int*)ctx->aux3.ptr;
+    double* d_out = nullptr;
+    const bool zc = P <= kZeroCopyMaxSets;
+    if (zc) {
+        // single options and small batches (DoubleHeston.pricing() calls): the kernel reads the
+        // inputs and writes the prices through pinned, mapped host memory -- one launch and one
+        // spin-wait instead of five staging copies, a read-back and a stream sync
+        const size_t need = pb + 3 * vb + (size_t)P * 4 + (size_t)P;
+        HIP_TRY(ctx->h_pairs.reserve(need));
+        char* h = (char*)ctx->h_pairs.ptr;
+        char* d = (char*)ctx->h_pairs.dptr;
+        std::memcpy(h, params, pb);
+        std::memcpy(h + pb, K, vb);
+        std::memcpy(h + pb + vb, T, vb);
+        int* perm = (int*)(h + pb + 3 * vb);
+        for (int64_t i = 0; i < P; ++i) perm[i] = (int)i;
+        std::memcpy(h + pb + 3 * vb + (size_t)P * 4, is_call, (size_t)P);
+        A.prm = (const double*)d;
+        A.K = (const double*)(d + pb);
+        A.T = (const double*)(d + pb + vb);
+        d_out = (double*)(d + pb + 2 * vb);
+        A.perm = (const int*)(d + pb + 3 * vb);
+        A.call = (const int8_t*)(d + pb + 3 * vb + (size_t)P * 4);
+    } else {
+        HIP_TRY(ctx->params.reserve(pb));
+        HIP_TRY(ctx->out.reserve(vb));
+        HIP_TRY(ctx->aux0.reserve(vb));
+        HIP_TRY(ctx->aux1.reserve(vb));
+        HIP_TRY(ctx->aux2.reserve((size_t)P));
+        HIP_TRY(ctx->aux3.reserve((size_t)P * 4));
+        std::vector<int> ident((size_t)P);
+        std::iota(ident.begin(), ident.end(), 0);
+        HIP_TRY(hipMemcpyAsync(ctx->params.ptr, params, pb, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->aux0.ptr, K, vb, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->aux1.ptr, T, vb, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->aux2.ptr, is_call, (size_t)P, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->aux3.ptr, ident.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));        // `ident` is pageable and leaves scope
+        A.prm = (const double*)ctx->params.ptr;
+        A.K = (const double*)ctx->aux0.ptr;
+        A.T = (const double*)ctx->aux1.ptr;
+        A.call = (const int8_t*)ctx->aux2.ptr;
+        A.perm = (const int*)ctx->aux3.ptr;
+        d_out = (double*)ctx->out.ptr;
+    }
     A.paired = 1;
     A.opt_cap = 2;
     A.max_group = 1;
@@ -2094,10 +2122,16 @@ int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const dou
     A.strike_mode = DH_STRIKE_ABSOLUTE;
     A.N = N;
     A.L = L;
-    A.out = (double*)ctx->out.ptr;
+    A.out = d_out;
     A.out_stride = 0;
     rc = launch_price(ctx, A, st);
     if (rc) return rc;
+    if (zc) {
+        rc = spin_sync(st);
+        if (rc) return rc;
+        std::memcpy(out, (char*)ctx->h_pairs.ptr + pb + 2 * vb, vb);
+        return DH_OK;
+    }
     HIP_TRY(hipMemcpyAsync(out, ctx->out.ptr, vb, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return DH_OK;

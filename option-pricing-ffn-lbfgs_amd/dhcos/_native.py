@@ -82,7 +82,7 @@ SIGNATURES = {
                                  C.c_double, _dp]),
     "dh_loss_batch": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp, _i8p, _dp, C.c_int, C.c_double,
                                 C.c_double, C.c_int, C.c_double, _dp, _i32p]),
-    "dh_price_pairs": (C.c_int, [_vp, _dp, _dp, _dp, _i8p, C.c_int64, C.c_int, C.c_double, _dp]),
+    "dh_price_pairs": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
     "dh_cos_coeffs": (C.c_int, [_vp, _i32p, C.c_int, C.c_double, C.c_double, C.c_double,
@@ -230,8 +230,8 @@ class Context:
         ic = np.ascontiguousarray(is_call, dtype=np.int8).reshape(P)
         out = np.empty(P)
         with self._lock:
-            _check(load().dh_price_pairs(self._h, _ptr(params), _ptr(K), _ptr(T), _ptr(ic, _i8p),
-                                         P, int(N), float(L), _ptr(out)))
+            _check(load().dh_price_pairs(self._h, params.ctypes.data, K.ctypes.data, T.ctypes.data,
+                                         ic.ctypes.data, P, int(N), float(L), out.ctypes.data))
         return out
 
     def price_batch(self, params, K, T, is_call, N=128, L=10.0):
@@ -261,6 +261,19 @@ class Context:
                                         _ptr(mkt), M, float(S0), float(r), int(N), float(L),
                                         _ptr(loss), _ptr(bad, _i32p)))
         return loss, bad
+
+    def price_one(self, rec16, K, T, is_call, N=128, L=10.0):
+        """One option under one param record (DoubleHeston.pricing): dh_price_pairs with P = 1,
+        raw addresses (the per-call marshalling is most of a single price's host cost)."""
+        rec = _f64(rec16)
+        kt = np.array([K, T])
+        ic = np.array([1 if is_call else 0], dtype=np.int8)
+        out = np.empty(1)
+        with self._lock:
+            _check(load().dh_price_pairs(self._h, rec.ctypes.data, kt.ctypes.data,
+                                         kt.ctypes.data + 8, ic.ctypes.data, 1, int(N), float(L),
+                                         out.ctypes.data))
+        return out[0]
 
     def cf(self, params16, u, tau):
         p = _f64(params16).reshape(PARAM_STRIDE)

@@ -77,8 +77,8 @@ class DoubleHeston:
     def pricing(self, N=128):
         """COS price with N terms -- double_heston.py:160-192."""
         is_call = resolve_call(self.option_type)
-        out = self._ctx().price_pairs(self._record()[None, :], [self.K], [self.T], [is_call], N)
-        return np.float64(out[0])
+        return np.float64(self._ctx().price_one(self._record(), float(self.K), float(self.T),
+                                                is_call, N))
 
     # -- batched entry point ----------------------------------------------------------------
     @staticmethod
