@@ -2610,6 +2610,13 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
     // chunk k, compacts the live starts (their requests are re-emitted at the new slots, in
     // stream order after chunk k + 1) and enqueues chunk k + 2.  Launches enqueued after the
     // last start finished return at once (live count 0).
+    struct DrainOnError {      // an early error return leaves no launch writing our buffers
+        hipStream_t st;
+        bool armed = true;
+        ~DrainOnError() {
+            if (armed) (void)hipStreamSynchronize(st);
+        }
+    } drain{st};
     const int chunk = opt->chunk > 0 ? opt->chunk : 8;
     const int64_t max_iters = (int64_t)opt->maxfun + 2LL * opt->maxls + 8;   // nfev bound per start
     std::vector<double> t_done(S, 0.0);
@@ -2674,6 +2681,7 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
     HIP_TRY(hipMemcpyAsync(hs.data(), ctx->lb_state.ptr, (size_t)S * sizeof(LbSlot),
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    drain.armed = false;
     for (int i = 0; i < S; ++i) {
         const LbSlot& q = hs[i];
         dh_lb_result& o = out[i];

@@ -450,7 +450,14 @@ DH_HD inline int lb_resume(LbCore<V, R>& c, const LbConfig& cf) {
     LbScalars& s = c.s;
     if (s.done) return 0;
     bool assign = s.task != kStart;                // START ignores f and g
-    for (;;) {
+    // Every pass either asks for a new point, records a NEW_X (bounded by maxiter) or finishes;
+    // passes that re-request the last evaluated point advance dcsrch, whose interval shrinks.
+    // The cap only guarantees the device loop ends whatever the inputs (NaN, say).
+    for (int guard = 0;; ++guard) {
+        if (guard > 4 * (cf.maxiter + cf.maxls) + 64) {
+            s.task = kErrorLs;
+            return lb_finish(s);
+        }
         if (assign) {
             s.f = s.fe;
             c.g = c.ge;
