@@ -60,6 +60,11 @@ constexpr size_t kTableBudget = size_t(256) << 20;   // table workspace per chun
 constexpr int kLdsMax = 160 * 1024;
 constexpr int kLdsDyn = kLdsMax - 4096;   // dynamic LDS cap: the kernels keep <= 4 KB static
 
+// Arrival counters of the loss hand-off, one per 128-byte line: every tile of a param set bumps
+// its set's counter with an agent-scope atomic, and packed counters put all the sets of a
+// request on one line, serialising every block's atomic (C2: 3.7k cycles per ticket).
+constexpr int kCounterStride = 32;
+
 struct PriceArgs {
     const double* prm;      // [P][16]
     int64_t P;              // param sets of the whole request
@@ -86,7 +91,7 @@ struct PriceArgs {
     int64_t out_stride;     // M (surface) or 0 (paired)
     double* part_sse;       // loss mode: [P*n_tiles] partials, else null
     int* part_bad;          // [P*n_tiles]
-    unsigned* counter;      // [P] arrival counters (zero between launches)
+    unsigned* counter;      // [P * kCounterStride] arrival counters (zero between launches)
     double* sse;            // [P] final sums (loss mode)
     int* n_bad;             // [P]
     double* table;          // workspace: [np*tabs_per_p][N] = w_k
@@ -554,6 +559,7 @@ __device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int 
 // of p with sc1 loads, the wave sums them in a fixed order and resets the counter.
 __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t task, int nopt,
                                           int t, const double* lsse, const double* lbad) {
+    DH_STAMP(A, 13);
     double s = 0.0, f = 0.0;
     for (int i = t; i < nopt; i += 64) {
         s += lsse[i];
@@ -563,13 +569,15 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
         s += __shfl_xor(s, off, 64);
         f += __shfl_xor(f, off, 64);
     }
+    DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
     unsigned old = 0;
     if (t == 0) {
         __hip_atomic_store(&A.part_sse[task], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&A.part_bad[task], (int)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        old = __hip_atomic_fetch_add(&A.counter[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        DH_STAMP(A, 15);
+        old = __hip_atomic_fetch_add(&A.counter[p * kCounterStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     old = __shfl(old, 0, 64);
     DH_STAMP(A, 12);
@@ -586,7 +594,7 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     if (t == 0) {
         A.sse[p] = acc;
         A.n_bad[p] = (int)bad;
-        __hip_atomic_store(&A.counter[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&A.counter[p * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1024,7 +1032,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
     __hip_atomic_store(&A.part_bad[task], (int)lbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old =
-        __hip_atomic_fetch_add(&A.counter[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&A.counter[p * kCounterStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old != (unsigned)A.n_tiles - 1u) return;
     const int64_t base_i = p * A.n_tiles;
     double acc = 0.0;
@@ -1035,7 +1043,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
     }
     A.sse[p] = acc;
     A.n_bad[p] = bad;
-    __hip_atomic_store(&A.counter[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&A.counter[p * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -1959,7 +1967,7 @@ static int surface_loss_launch(dh_ctx* ctx, const dh_surface* s, const double* d
     HIP_TRY(ctx->part_sse.reserve(nparts * 8));
     HIP_TRY(ctx->part_bad.reserve(nparts * 4));
     const size_t cap0 = ctx->counter.cap;
-    HIP_TRY(ctx->counter.reserve((size_t)S * 4));
+    HIP_TRY(ctx->counter.reserve((size_t)S * kCounterStride * 4));
     if (ctx->counter.cap != cap0) {       // fresh counters start at zero; kernels self-reset
         HIP_TRY(hipMemsetAsync(ctx->counter.ptr, 0, ctx->counter.cap, st));
     }

@@ -74,7 +74,8 @@ def main():
         print(f"  lifetime median {np.median(life):8.0f}  max {life.max():8.0f}")
         detail = [("prologue (thread 0)", 0, 8), ("staging wait", 8, 1), ("sums: setup", 3, 9),
                   ("sums: angle loop", 9, 10), ("sums: butterfly", 10, 11),
-                  ("sums: finalise", 11, 4), ("loss: to atomic", 4, 12), ("loss: last", 12, 5)]
+                  ("sums: finalise", 11, 4), ("loss: barrier", 4, 13), ("loss: wave sums", 13, 14),
+                  ("loss: store drain", 14, 15), ("loss: ticket", 15, 12), ("loss: last", 12, 5)]
         for nm, i0, i1 in detail:
             c = st[:, i1] - st[:, i0]
             print(f"    {nm:20s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}")
