@@ -1058,7 +1058,9 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
 // ----------------------------------------------------------------------------------------------
 template <int TPT1>
 __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(PriceArgs A, int tpt2) {
-    if (halted(A)) return;
+    // the halt test waits on a global load: taken after the staging barrier, so the load
+    // overlaps the prologue instead of delaying it (a halted launch wastes the prologue only)
+    const bool halt = halted(A);
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ double shc[kTabC];
     __shared__ double red[4][1];
@@ -1107,6 +1109,7 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
         L.exK[i] = ratio;
     }
     __syncthreads();
+    if (halt) return;                              // uniform: every block reads the same count
     DH_STAMP(A, 1);
 
     const double a = shc[0], b = shc[1], eb = shc[2], ea = shc[3], scale = shc[4], piba = shc[5];
@@ -2338,6 +2341,8 @@ struct LbSlot {
     dhlb::LbScalars s;
 };
 
+constexpr int kLbInline = 64;   // live lists up to this size travel in the kernel arguments
+
 struct LbArgs {
     LbSlot* states;            // [S]
     const int* live;           // [n_live] start index of each slot
@@ -2354,6 +2359,8 @@ struct LbArgs {
     double S0, r;
     int M;
     int mode;                  // 0 begin at x0, 1 consume the request and advance, 2 re-emit
+    int n_inline;              // live list passed by value below (saves a dependent load), or 0
+    int live_inline[kLbInline];
 };
 
 __device__ __forceinline__ WaveVec lb_ld(const LbSlot* g, int v, int lane) {
@@ -2418,7 +2425,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     [[maybe_unused]] const unsigned long long t_start = lb_clock();
     const int slot = blockIdx.x;
     const int lane = threadIdx.x;
-    const int sidx = A.live[slot];
+    const int sidx = A.n_inline ? A.live_inline[slot] : A.live[slot];
     LbSlot* G = A.states + sidx;
     WaveCore c;
     [[maybe_unused]] unsigned long long t_load = 0, t_req = 0, t_sm = 0;
@@ -2610,6 +2617,11 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
     A.r = r;
     A.M = s->M;
     A.mode = 0;
+    auto set_inline = [&](const int* lst, int n) {
+        A.n_inline = n <= kLbInline ? 1 : 0;
+        for (int i = 0; i < kLbInline; ++i) A.live_inline[i] = i < n && A.n_inline ? lst[i] : 0;
+    };
+    set_inline(h_live[0], S);
     rc = launch_lb_step(st, A, S);
     if (rc) return rc;
 
@@ -2674,10 +2686,13 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
         if (next.size() != live.size()) {              // compact; re-emit their requests
             live.swap(next);
             n_live = (int)live.size();
-            int* hl = h_live[(k + 1) & 1];             // the other buffer's upload has run
-            std::memcpy(hl, live.data(), (size_t)n_live * 4);
-            HIP_TRY(hipMemcpyAsync(ctx->lb_live.ptr, hl, (size_t)n_live * 4,
-                                   hipMemcpyHostToDevice, st));
+            set_inline(live.data(), n_live);
+            if (!A.n_inline) {
+                int* hl = h_live[(k + 1) & 1];         // the other buffer's upload has run
+                std::memcpy(hl, live.data(), (size_t)n_live * 4);
+                HIP_TRY(hipMemcpyAsync(ctx->lb_live.ptr, hl, (size_t)n_live * 4,
+                                       hipMemcpyHostToDevice, st));
+            }
             A.mode = 2;
             rc = launch_lb_step(st, A, n_live);
             if (rc) return rc;
