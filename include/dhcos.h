@@ -117,6 +117,15 @@ int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params
                         double L, double* d_sse, int32_t* d_n_bad, double* d_prices,
                         void* stream);
 
+/* One function+gradient request per start for a host-driven optimizer (the SciPy driver):
+ * x0[S][13] unconstrained -> f[S] = compute_loss(x0) (lbfgs_calibrator.py:118-177), g[S][13] =
+ * SciPy's 2-point forward difference (loss(x0 + h_i e_i) - f) / ((x0_i + h_i) - x0_i) with
+ * h = 1e-8 (scipy/optimize/_numdiff.py:498-511,592-596), low[S] = the smallest valid loss of the
+ * 14 points (best_loss, :171-172).  The 14 x S records are formed on the host and priced in one
+ * request (dh_surface_loss).                                                                   */
+int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0, int S, double S0, double r,
+                  int N, double L, double* f, double* g, double* low);
+
 /* ---- device-resident multi-start L-BFGS-B ------------------------------------------------- */
 /* Runs S independent L-BFGS-B starts (no bounds) on the surface's calibration loss without a
  * host round trip per iteration.  Replaces the per-start

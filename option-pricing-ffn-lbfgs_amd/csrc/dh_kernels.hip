@@ -2847,3 +2847,63 @@ extern "C" int dh_loss_batch(dh_ctx* ctx, const double* x, int S, const double* 
     dh_surface_destroy(s);
     return rc;
 }
+
+// ----------------------------------------------------------------------------------------------
+// function + FD-gradient requests for the host (SciPy) driver
+// ----------------------------------------------------------------------------------------------
+extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0, int S, double S0,
+                             double r, int N, double L, double* f, double* g, double* low) {
+    if (!ctx || !s || (S > 0 && (!x0 || !f || !g || !low))) return fail(DH_E_ARG, "null argument");
+    if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
+    if (s->M == 0) return fail(DH_E_ARG, "empty market (the loss is NaN)");
+    if (S < 0) return fail(DH_E_ARG, "S < 0");
+    if (S == 0) return DH_OK;
+    constexpr int kP = dhlb::kPts, kN = dhlb::kN;
+    const size_t P = (size_t)S * kP;
+    std::vector<double> rec(P * DH_PARAM_STRIDE), pen(P), dx((size_t)S * kN), sse(P);
+    std::vector<int32_t> bad(P);
+    // the request's points (scipy/optimize/_numdiff.py:498-511: x0, then x0 + h_i e_i with
+    // h = 1e-8, or sqrt(eps) sign(x) max(1, |x|) where the absolute step vanishes), their model
+    // params (exp / tanh / identity, lbfgs_calibrator.py:62-87) and Feller penalties (:113-116)
+    for (int st = 0; st < S; ++st) {
+        const double* x = x0 + (size_t)st * kN;
+        double pb[kN], pp[kN];
+        for (int i = 0; i < kN; ++i) {
+            double h = kFdStep;
+            if ((x[i] + h) - x[i] == 0.0)
+                h = kSqrtEps * (x[i] >= 0.0 ? 1.0 : -1.0) * std::max(1.0, std::fabs(x[i]));
+            const double xh = x[i] + h;
+            dx[(size_t)st * kN + i] = xh - x[i];
+            const bool th = i == 4 || i == 9, id = i == 11;
+            pb[i] = th ? std::tanh(x[i]) : (id ? x[i] : std::exp(x[i]));
+            pp[i] = th ? std::tanh(xh) : (id ? xh : std::exp(xh));
+        }
+        for (int t = 0; t < kP; ++t) {
+            double* o = rec.data() + ((size_t)st * kP + t) * DH_PARAM_STRIDE;
+            for (int i = 0; i < kN; ++i) o[i] = (i == t - 1) ? pp[i] : pb[i];
+            const double v1 = o[3] * o[3] - 2.0 * o[1] * o[2];
+            const double v2 = o[8] * o[8] - 2.0 * o[6] * o[7];
+            pen[(size_t)st * kP + t] = 1000.0 * ((v1 > 0.0 ? v1 : 0.0) + (v2 > 0.0 ? v2 : 0.0));
+            o[13] = S0;
+            o[14] = r;
+            o[15] = 0.0;
+        }
+    }
+    int rc = dh_surface_loss(ctx, s, rec.data(), (int)P, N, L, sse.data(), bad.data(), nullptr);
+    if (rc) return rc;
+    // loss = n_bad ? 1e10 : sse / M + Feller (lbfgs_calibrator.py:152-166); f, the FD gradient
+    // (f_i - f_0) / dx_i as SciPy forms it, and the smallest valid loss of the request
+    for (int st = 0; st < S; ++st) {
+        double lo = __builtin_huge_val(), fl[kP];
+        for (int t = 0; t < kP; ++t) {
+            const size_t i = (size_t)st * kP + t;
+            fl[t] = bad[i] > 0 ? kInvalidLoss : sse[i] / (double)s->M + pen[i];
+            if (fl[t] == fl[t] && fl[t] != kInvalidLoss && fl[t] < lo) lo = fl[t];
+        }
+        f[st] = fl[0];
+        low[st] = lo;
+        for (int i = 0; i < kN; ++i)
+            g[(size_t)st * kN + i] = (fl[i + 1] - fl[0]) / dx[(size_t)st * kN + i];
+    }
+    return DH_OK;
+}

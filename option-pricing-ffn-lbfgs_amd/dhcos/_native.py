@@ -82,6 +82,8 @@ SIGNATURES = {
                                  C.c_double, _dp]),
     "dh_loss_batch": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp, _i8p, _dp, C.c_int, C.c_double,
                                 C.c_double, C.c_int, C.c_double, _dp, _i32p]),
+    "dh_surface_fg": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_double, C.c_double, C.c_int,
+                                C.c_double, _vp, _vp, _vp]),
     "dh_price_pairs": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
@@ -375,6 +377,17 @@ class Surface:
                                              float(r), int(N), float(L), C.byref(opt), res,
                                              C.byref(nl)))
         return list(res)[:S], nl.value
+
+    def fg(self, X0, S0, r, N=128, L=10.0):
+        """dh_surface_fg: (f [S], g [S, 13], low [S]) of one FD request per row of X0 [S, 13]."""
+        X0 = _f64(X0).reshape(-1, 13)
+        S = X0.shape[0]
+        f, g, low = np.empty(S), np.empty((S, 13)), np.empty(S)
+        with self.ctx._lock:
+            _check(load().dh_surface_fg(self.ctx.handle, self._h, X0.ctypes.data, S, float(S0),
+                                        float(r), int(N), float(L), f.ctypes.data, g.ctypes.data,
+                                        low.ctypes.data))
+        return f, g, low
 
     # device-pointer variants (torch tensors or raw device addresses)
     def price_dev(self, d_params: int, P: int, d_out: int, N=128, L=10.0, stream: int = 0):

@@ -103,6 +103,17 @@ def fd_request_points(x0, h=FD_ABS_STEP):
 _SQRT_EPS = float(np.sqrt(np.finfo(np.float64).eps))
 
 
+def fg_from_losses(cal, X0):
+    """fg_batch through ``cal.loss_batch``: the 14 points of each request, their losses, SciPy's
+    forward difference and the smallest valid loss (NaN never wins, 1e10 is not valid)."""
+    S = X0.shape[0]
+    X, dx = fd_request_points_many(X0)
+    F = cal.loss_batch(X, track=False).reshape(S, N_PARAMS + 1)
+    G = (F[:, 1:] - F[:, :1]) / dx
+    low = np.min(np.where((F == INVALID_LOSS) | np.isnan(F), np.inf, F), axis=1)
+    return F[:, 0].copy(), G, low
+
+
 def fd_request_points_many(X0, h=FD_ABS_STEP):
     """fd_request_points for every row of X0 [S, n]: -> X [S * (n + 1), n] (per start x0 then
     x0 + h_i e_i, start-major) and dx [S, n].  Elementwise the same arithmetic."""
@@ -208,6 +219,20 @@ class DoubleHestonJumpCalibrator:
                 if lo < self.best_loss:
                     self.best_loss = lo
         return loss
+
+    def fg_batch(self, X0: np.ndarray):
+        """One SciPy function+gradient request per row of X0 [S, 13] in one launch:
+        -> (f [S], g [S, 13], low [S] = smallest valid loss of each request's 14 points).
+        Natively (dh_surface_fg: FD points, transforms, Feller and the gradient formed in C++
+        around one loss request) unless a subclass replaces loss_batch, whose values are then
+        used the same way."""
+        X0 = np.atleast_2d(np.asarray(X0, dtype=np.float64))
+        native = type(self).loss_batch is DoubleHestonJumpCalibrator.loss_batch
+        surf = self._get_surface() if native and len(self.market_options) else None
+        if surf is None:
+            return fg_from_losses(self, X0)
+        self.loss_evals += X0.shape[0] * (N_PARAMS + 1)
+        return surf.fg(X0, self.spot, self.risk_free_rate, self.N)
 
     def compute_loss(self, x: np.ndarray) -> float:
         """Relative MSE + Feller penalty (lbfgs_calibrator.py:118-177)."""
@@ -443,9 +468,10 @@ def _advance(cal, gens, states, order, outcomes):
             pending[sid] = next(gens[sid])
         while pending:
             ids = sorted(pending)
-            X, dx = fd_request_points_many(np.stack([pending[sid] for sid in ids]))
             try:
-                f = cal.loss_batch(X, track=False)
+                X0 = np.stack([pending[sid] for sid in ids])
+                f0, G, lows = (cal.fg_batch(X0) if hasattr(cal, "fg_batch")
+                               else fg_from_losses(cal, X0))
             except _native.NativeError:
                 raise
             except Exception:          # reference: except -> continue (the start is dropped)
@@ -454,17 +480,14 @@ def _advance(cal, gens, states, order, outcomes):
                 pending.clear()
                 break
             launches += 1
-            F = f.reshape(len(ids), N_PARAMS + 1)
-            G = (F[:, 1:] - F[:, :1]) / dx
             # per-start best valid loss (NaN never wins, 1e10 is not a valid loss)
-            lows = np.min(np.where((F == INVALID_LOSS) | np.isnan(F), np.inf, F), axis=1)
             for j, sid in enumerate(ids):
                 st = states[sid]
                 st.n_calls += N_PARAMS + 1
                 if lows[j] < st.best_loss:
                     st.best_loss = lows[j]
                 try:
-                    pending[sid] = gens[sid].send((F[j, 0], G[j]))
+                    pending[sid] = gens[sid].send((f0[j], G[j]))
                 except StopIteration as stop:
                     outcomes[sid] = (stop.value, time.time())
                     del pending[sid]
