@@ -2239,7 +2239,9 @@ constexpr double kInvalidLoss = 1e10;                 // lbfgs_calibrator.py:152
 constexpr double kFdStep = 1e-8;                      // SciPy L-BFGS-B eps
 constexpr double kSqrtEps = 1.4901161193847656e-08;   // sqrt(DBL_EPSILON), _numdiff fallback
 
-// A 13-vector held one component per lane (lanes 13..63 hold 0).  Reductions are DPP
+// A 13-vector held one component per lane of each 16-lane row (lane l holds component l & 15;
+// components 13..15 are 0): the four rows are copies, so every lane computes the same scalars
+// and the state machine's branches are uniform across the wave.  Reductions are DPP
 // butterflies inside each 16-lane row -- quad_perm [1,0,3,2], quad_perm [2,3,0,1],
 // row_half_mirror, row_mirror -- in which both partners add the same two operands, so every lane
 // of the row ends with the same bits: the pairwise tree ((p0+p1)+(p2+p3)) + ... that
@@ -2291,8 +2293,8 @@ struct WaveRing {
     double* rdr;               // [kM] rho_j = 1 / dr_j
     double* ra;                // [kM]
     int lane;
-    __device__ WaveVec s(int j) const { return {lane < dhlb::kLanes ? rs[j * dhlb::kLanes + lane] : 0.0}; }
-    __device__ WaveVec y(int j) const { return {lane < dhlb::kLanes ? ry[j * dhlb::kLanes + lane] : 0.0}; }
+    __device__ WaveVec s(int j) const { return {rs[j * dhlb::kLanes + (lane & 15)]}; }
+    __device__ WaveVec y(int j) const { return {ry[j * dhlb::kLanes + (lane & 15)]}; }
     __device__ double rho(int j) const { return rdr[j]; }
     __device__ double& a(int j) { return ra[j]; }
     __device__ void put(int j, WaveVec sj, WaveVec yj, double d) {
@@ -2364,7 +2366,7 @@ struct LbArgs {
 };
 
 __device__ __forceinline__ WaveVec lb_ld(const LbSlot* g, int v, int lane) {
-    return {lane < dhlb::kLanes ? g->vec[v][lane] : 0.0};
+    return {g->vec[v][lane & 15]};
 }
 
 __device__ __forceinline__ void lb_st(LbSlot* g, int v, int lane, WaveVec x) {
@@ -2379,22 +2381,23 @@ __device__ __forceinline__ double lb_transform(int i, double x) {
     return exp(x);
 }
 
-// Emit the pending request at xe.  Lane i < 13 maps x_i and x_i + h_i (SciPy's step rule,
-// scipy/optimize/_numdiff.py:498-511) to model params and keeps dx_i = (x_i + h_i) - x_i; lane
-// t < 14 assembles point t (x, or x + h_{t-1} e_{t-1}), writes its record and keeps its Feller
-// penalty (lbfgs_calibrator.py:113-116) in pen.
+// Emit the pending request at xe.  Lanes i and 16 + i (i < 13) form x_i + h_i (SciPy's step rule,
+// scipy/optimize/_numdiff.py:498-511); lane i maps x_i and lane 16 + i maps x_i + h_i to a model
+// param (one transform per lane), lane i keeps dx_i = (x_i + h_i) - x_i; lane t < 14 assembles
+// point t (x, or x + h_{t-1} e_{t-1}), writes its record and keeps its Feller penalty
+// (lbfgs_calibrator.py:113-116) in pen.
 __device__ void lb_emit(const WaveCore& c, WaveVec& dx, WaveVec& pen, double* pb, double* pp,
                         const LbArgs& A, int slot, int lane) {
-    if (lane < dhlb::kN) {
-        const double xi = c.xe.v;
-        double h = kFdStep;
-        if ((xi + h) - xi == 0.0) h = kSqrtEps * (xi >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(xi));
-        const double xh = xi + h;
-        dx.v = xh - xi;
-        pb[lane] = lb_transform(lane, xi);
-        pp[lane] = lb_transform(lane, xh);
-    } else {
-        dx.v = 0.0;
+    const int i = lane & 15;
+    const double xi = c.xe.v;                       // every row holds xe
+    double h = kFdStep;
+    if ((xi + h) - xi == 0.0) h = kSqrtEps * (xi >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(xi));
+    const double xh = xi + h;
+    dx.v = i < dhlb::kN ? xh - xi : 0.0;
+    if (lane < 32 && i < dhlb::kN) {
+        const double v = lb_transform(i, lane < 16 ? xi : xh);
+        if (lane < 16) pb[i] = v;
+        else pp[i] = v;
     }
     __syncthreads();
     pen.v = 0.0;
@@ -2439,15 +2442,16 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
         const WaveVec z{0.0};
         c.x = c.g = c.z = c.d = c.t = c.r = c.ge = z;
         for (int i = lane; i < kLbRing + dhlb::kM; i += 64) ring[i] = 0.0;
-        const WaveVec x0{lane < dhlb::kN ? A.x0[(size_t)sidx * dhlb::kN + lane] : 0.0};
+        const int li = lane & 15;
+        const WaveVec x0{li < dhlb::kN ? A.x0[(size_t)sidx * dhlb::kN + li] : 0.0};
         dhlb::lb_begin(c, x0);
         c.s.best_loss = __builtin_huge_val();
         c.s.n_calls = 0;
     } else {
         // every load is issued before any is used (one memory round trip): the finished request's
         // loss terms, the pair memory, the vectors and the scalars
-        if (A.mode == 1 && lane < dhlb::kPts) {
-            const size_t i = (size_t)slot * dhlb::kPts + lane;
+        if (A.mode == 1 && (lane & 15) < dhlb::kPts) {
+            const size_t i = (size_t)slot * dhlb::kPts + (lane & 15);
             req_sse = A.sse[i];
             req_bad = A.bad[i];
         }
@@ -2480,14 +2484,14 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     if (A.mode == 1) {
         t_load = lb_clock();
         double f = __builtin_huge_val();
-        if (lane < dhlb::kPts) f = req_bad > 0 ? kInvalidLoss : req_sse / (double)A.M + pen.v;
+        if ((lane & 15) < dhlb::kPts) f = req_bad > 0 ? kInvalidLoss : req_sse / (double)A.M + pen.v;
         if (lane < dhlb::kLanes) fl[lane] = f;
         __syncthreads();
         const double lo = row_min((f == f && f != kInvalidLoss) ? f : __builtin_huge_val());
         c.s.n_calls += dhlb::kPts;
         if (lo < c.s.best_loss) c.s.best_loss = lo;
         c.s.fe = fl[0];
-        c.ge.v = lane < dhlb::kN ? (fl[lane + 1] - fl[0]) / dx.v : 0.0;
+        c.ge.v = (lane & 15) < dhlb::kN ? (fl[(lane & 15) + 1] - fl[0]) / dx.v : 0.0;
         if (A.trace) {
             unsigned long long k = 0;
             if (lane == 0) k = atomicAdd(A.trace_n, 1ull);
