@@ -164,20 +164,23 @@ DH_HD inline void dcstep(double& stx, double& fx, double& dx, double& sty, doubl
             stpf = stpmin;
         }
     }
-    if (fp > fx) {
-        sty = stp;
-        fy = fp;
-        dy = dp;
-    } else {
-        if (sgnd < 0.0) {
-            sty = stx;
-            fy = fx;
-            dy = dx;
-        }
-        stx = stp;
-        fx = fp;
-        dx = dp;
-    }
+    // the interval update as selects with every output written once (conditional stores to
+    // different references are sunk by the compiler into a store through a selected pointer,
+    // which keeps the line-search state in scratch memory on the device)
+    const bool hi = fp > fx;
+    const bool swap = !hi && sgnd < 0.0;
+    const double nsty = hi ? stp : (swap ? stx : sty);
+    const double nfy = hi ? fp : (swap ? fx : fy);
+    const double ndy = hi ? dp : (swap ? dx : dy);
+    const double nstx = hi ? stx : stp;
+    const double nfx = hi ? fx : fp;
+    const double ndx = hi ? dx : dp;
+    sty = nsty;
+    fy = nfy;
+    dy = ndy;
+    stx = nstx;
+    fx = nfx;
+    dx = ndx;
     stp = stpf;
 }
 
@@ -223,21 +226,37 @@ DH_HD inline void dcsrch(LsState& ls, double f, double g, double& stp, double st
         ls.task = task;
         return;
     }
-    if (ls.stage == 1 && f <= ls.fx && f > ftest) {
-        const double fm = f - stp * ls.gtest;
-        double fxm = ls.fx - ls.stx * ls.gtest;
-        double fym = ls.fy - ls.sty * ls.gtest;
-        const double gm = g - ls.gtest;
-        double gxm = ls.gx - ls.gtest;
-        double gym = ls.gy - ls.gtest;
-        dcstep(ls.stx, fxm, gxm, ls.sty, fym, gym, stp, fm, gm, ls.brackt, ls.stmin, ls.stmax);
+    // one dcstep call site on locals (two call sites binding different references were merged
+    // by the compiler into one through pointer selects, which kept the line-search state in
+    // scratch memory on the device)
+    const bool modified = ls.stage == 1 && f <= ls.fx && f > ftest;
+    double fm, gm, fxm, gxm, fym, gym;
+    if (modified) {                      // the modified function psi = f - stp gtest
+        fm = f - stp * ls.gtest;
+        fxm = ls.fx - ls.stx * ls.gtest;
+        fym = ls.fy - ls.sty * ls.gtest;
+        gm = g - ls.gtest;
+        gxm = ls.gx - ls.gtest;
+        gym = ls.gy - ls.gtest;
+    } else {
+        fm = f;
+        fxm = ls.fx;
+        fym = ls.fy;
+        gm = g;
+        gxm = ls.gx;
+        gym = ls.gy;
+    }
+    dcstep(ls.stx, fxm, gxm, ls.sty, fym, gym, stp, fm, gm, ls.brackt, ls.stmin, ls.stmax);
+    if (modified) {
         ls.fx = fxm + ls.stx * ls.gtest;
         ls.fy = fym + ls.sty * ls.gtest;
         ls.gx = gxm + ls.gtest;
         ls.gy = gym + ls.gtest;
     } else {
-        dcstep(ls.stx, ls.fx, ls.gx, ls.sty, ls.fy, ls.gy, stp, f, g, ls.brackt, ls.stmin,
-               ls.stmax);
+        ls.fx = fxm;
+        ls.fy = fym;
+        ls.gx = gxm;
+        ls.gy = gym;
     }
     if (ls.brackt) {
         if (fabs(ls.sty - ls.stx) >= p66 * ls.width1) stp = ls.stx + p5 * (ls.sty - ls.stx);
