@@ -1,0 +1,44 @@
+"""bench.py's output contract (the driver parses its last line): one JSON object with the metric
+and unit of BASELINE.json, the whole-job value, the timing fields, config.workload, the roofline
+object and -- on rank 0 at N = 1 -- the CPU baseline object.  Runs a short C1 bench on the GPU
+(a child process, as the driver runs it); the CPU baseline leg gets a 1 s budget."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.mark.gpu
+def test_bench_line_contract():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c1", "--steps", "5",
+           "--warmup", "2", "--no-calib", "--cpu-budget", "1", "--cpu-cores", "2"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                "roofline", "cpu_baseline"):
+        assert key in line, key
+    assert line["metric"].startswith("option-prices/sec") and base["metric"].startswith(
+        "option-prices/sec")
+    assert line["unit"] == "option-prices/s" and line["value"] > 0
+    assert (line["n_gpus"], line["steps"], line["warmup"]) == (1, 5, 2)
+    assert line["higher_is_better"] is True and line["scaling"] in ("weak", "strong")
+    assert line["vs_baseline"] is None and line["dtype"] == "f64"
+    assert "workload" in line["config"]
+    # value = prices of one step / step time (ms_per_step in milliseconds)
+    per_step = line["config"]["prices_per_step"]
+    assert abs(line["value"] * line["ms_per_step"] * 1e-3 - per_step) <= 1e-6 * per_step
+    r = line["roofline"]
+    for key in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert key in r, key
+    assert r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    c = line["cpu_baseline"]
+    assert c["kind"] in ("port", "reference") and c["value"] > 0 and c["cores"] == 2
+    assert c["sample"]
