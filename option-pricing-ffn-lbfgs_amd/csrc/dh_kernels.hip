@@ -84,6 +84,8 @@ struct PriceArgs {
     int paired;             // option i under param set i, one option per task
     int strike_mode;
     int exact;              // validation mode (host routes to cos_exact_kernel)
+    int partials_only;      // loss requests of the device L-BFGS-B: every task stores its partial
+                            // and ends (no hand-off); the step kernel forms the sums
     int M;                  // options in the (sorted) option arrays
     int N;
     double L;
@@ -571,6 +573,11 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     }
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
+    if (A.partials_only) {          // plain stores: the next launch (the step kernel) reads them;
+        if (t == 0)                 // a tile with an invalid price stores NaN (the set's loss is then
+            A.part_sse[task] = f > 0.0 ? __builtin_nan("") : s;   // 1e10 whatever its sum)
+        return;
+    }
     unsigned old = 0;
     if (t == 0) {
         __hip_atomic_store(&A.part_sse[task], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1647,6 +1654,7 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     }
     for (int64_t p0 = 0; p0 < A0.P; p0 += chunk) {
         PriceArgs A = A0;
+        A.partials_only = 0;        // the split kernels always finish the loss hand-off
         A.p0 = p0;
         A.np = std::min<int64_t>(chunk, A0.P - p0);
         A.table = (double*)ctx->table.ptr;
@@ -1950,7 +1958,8 @@ int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_param
 
 static int surface_loss_launch(dh_ctx* ctx, const dh_surface* s, const double* d_params, int S,
                                int N, double L, double* d_sse, int32_t* d_n_bad,
-                               double* d_prices, void* stream, const int* live_count) {
+                               double* d_prices, void* stream, const int* live_count,
+                               bool partials_only = false) {
     if (!ctx || !s || (S > 0 && (!d_params || !d_sse || !d_n_bad)))
         return fail(DH_E_ARG, "null argument");
     if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
@@ -1983,6 +1992,7 @@ static int surface_loss_launch(dh_ctx* ctx, const dh_surface* s, const double* d
     A.sse = d_sse;
     A.n_bad = (int*)d_n_bad;
     A.live_count = live_count;
+    A.partials_only = partials_only && !A.exact ? 1 : 0;
     return launch_price(ctx, A, st);
 }
 
@@ -2361,6 +2371,10 @@ struct LbArgs {
     double S0, r;
     int M;
     int mode;                  // 0 begin at x0, 1 consume the request and advance, 2 re-emit
+    int part_mode;             // 1: the request ran fused with partials_only -- sum its tile
+                               // partials here (the hand-off's order); 0: read sse / bad
+    const double* part_sse;    // [n_live * 14][n_tiles] (part_mode 1; NaN: invalid price)
+    int n_tiles;
     int n_inline;              // live list passed by value below (saves a dependent load), or 0
     int live_inline[kLbInline];
 };
@@ -2417,6 +2431,37 @@ __device__ void lb_emit(const WaveCore& c, WaveVec& dx, WaveVec& pen, double* pb
     }
 }
 
+// The loss hand-off's sum of one param set's nt tile partials (task_loss: lane l adds tiles l,
+// l + 64, ... in order, then an xor butterfly), formed by one lane: leaf l as that lane's sum,
+// then the butterfly's tree (level w adds leaves w apart).  Leaves past nt are +0.0 and adding
+// +0.0 to a partial (a sum of squares) changes no bit, so W = 16 or 32 leaves give the 64-leaf
+// tree's bits.  Loads are clamped in-bounds and issued before any add.  A tile with an invalid
+// price stored NaN instead of its partial, and a NaN sum marks the set invalid (its loss is 1e10
+// whatever the sum; a valid sum is never NaN: its terms are squares, at worst +inf).
+template <int W>
+__device__ __forceinline__ void lb_tile_tree(const double* ps, int nt, double& sse, int& bad) {
+    double x[W];
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+        const double v = ps[min(u, nt - 1)];
+        x[u] = 0.0 + (u < nt ? v : 0.0);
+    }
+    for (int j0 = W; j0 < nt; j0 += W) {          // W = 64 only
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+            const double v = ps[min(j0 + u, nt - 1)];
+            x[u] += j0 + u < nt ? v : 0.0;
+        }
+    }
+#pragma unroll
+    for (int w = 1; w < W; w <<= 1) {
+#pragma unroll
+        for (int u = 0; u < W; u += 2 * w) x[u] = x[u] + x[u + w];
+    }
+    sse = x[0];
+    bad = isnan(x[0]) ? 1 : 0;                     // a tile stored NaN: an invalid price
+}
+
 // One wave per live start: load the state (vectors into registers, lane i = component i; the
 // pair memory into LDS), consume the finished request (lane t forms loss t, lane i gradient
 // component i), run the L-BFGS-B state machine until it needs a new point, emit that request,
@@ -2450,7 +2495,18 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     } else {
         // every load is issued before any is used (one memory round trip): the finished request's
         // loss terms, the pair memory, the vectors and the scalars
-        if (A.mode == 1 && (lane & 15) < dhlb::kPts) {
+        if (A.mode == 1 && A.part_mode) {
+            // the loss hand-off's sum (task_loss), formed by lane t of every row for point t
+            // (lb_tile_tree: the same additions, so the same bits)
+            const int li = lane & 15;
+            if (li < dhlb::kPts) {
+                const int nt = A.n_tiles;
+                const double* ps = A.part_sse + ((size_t)slot * dhlb::kPts + li) * nt;
+                if (nt <= 16) lb_tile_tree<16>(ps, nt, req_sse, req_bad);
+                else if (nt <= 32) lb_tile_tree<32>(ps, nt, req_sse, req_bad);
+                else lb_tile_tree<64>(ps, nt, req_sse, req_bad);
+            }
+        } else if (A.mode == 1 && (lane & 15) < dhlb::kPts) {
             const size_t i = (size_t)slot * dhlb::kPts + (lane & 15);
             req_sse = A.sse[i];
             req_bad = A.bad[i];
@@ -2621,6 +2677,8 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
     A.r = r;
     A.M = s->M;
     A.mode = 0;
+    A.part_mode = 0;
+    A.n_tiles = s->n_tiles;
     auto set_inline = [&](const int* lst, int n) {
         A.n_inline = n <= kLbInline ? 1 : 0;
         for (int i = 0; i < kLbInline; ++i) A.live_inline[i] = i < n && A.n_inline ? lst[i] : 0;
@@ -2650,8 +2708,11 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
         A.mode = 1;
         for (int c = 0; c < chunk; ++c) {
             int e = surface_loss_launch(ctx, s, A.rec, n_live * dhlb::kPts, N, L, (double*)A.sse,
-                                        (int32_t*)A.bad, nullptr, st, A.live_count);
+                                        (int32_t*)A.bad, nullptr, st, A.live_count, true);
             if (e) return e;
+            // a fused request stored its tile partials only (no hand-off): the step sums them
+            A.part_mode = !ctx->exact && ctx->last_path == DH_PATH_FUSED ? 1 : 0;
+            A.part_sse = (const double*)ctx->part_sse.ptr;
             e = launch_lb_step(st, A, n_live);
             if (e) return e;
             ++launches;

@@ -10,6 +10,9 @@ import sys
 
 import numpy as np
 import pytest
+# torch before the first libdhcos call: both then bind one HIP runtime (dhcos/_native.py), in
+# whatever order the GPU tests run
+import torch  # noqa: F401
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "option-pricing-ffn-lbfgs_amd")

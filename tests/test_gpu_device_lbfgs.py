@@ -147,6 +147,21 @@ def test_device_replays_bitwise_on_cpu_build(dh, calib_golden):
         assert list(info) == [r.nit, r.nfev, r.task, r.warnflag]
 
 
+def test_invalid_prices_mark_the_loss_on_both_drivers(dh, calib_golden):
+    """A start whose prices are invalid (v0 = e^40 overflows the CF: NaN prices) has loss 1e10 at
+    every point (lbfgs_calibrator.py:152-158).  The device driver's loss requests store a NaN
+    partial for such a tile instead of the hand-off's bad count; both drivers must end the same
+    way: ABNORMAL at x0 with fun = 1e10 and the same request count."""
+    from dhcos.calibrator import run_starts, run_starts_device
+    x0 = np.array(calib_golden["calibrate_seed0_starts"][0]["x0"], dtype=float)
+    x0[0] = x0[5] = 40.0
+    (dev, _), = run_starts_device(_cal(dh, calib_golden), [x0], 300)
+    (host, _), = run_starts(_cal(dh, calib_golden), [x0], 300)
+    assert dev.fun == host.fun == 1e10
+    assert (dev.nit, dev.nfev, dev.message) == (host.nit, host.nfev, host.message)
+    assert np.array_equal(dev.x, host.x) and np.array_equal(dev.x, x0)
+
+
 def test_degenerate_markets_fall_back_to_reference_semantics(dh, calib_golden):
     """'' option type (every loss 1e10) and an empty market (NaN) have nothing to optimise; the
     device driver hands them to the host driver and returns the reference's result."""
