@@ -201,8 +201,9 @@ CONFIGS = {
 def calib_leg(S0, r, opts, N, n_starts, world, coll, driver):
     """Time calibrate(maxiter=300, multi_start=n_starts) under np.random.seed(0) (starts
     sharded over the ranks at N > 1) with the given optimizer driver; max over ranks."""
-    # untimed warm-up of the same driver (first-call costs: BLAS pool, surface upload paths)
-    DoubleHestonJumpCalibrator(S0, r, opts, N=N).calibrate(maxiter=2, multi_start=1,
+    # untimed warm-up of the same driver with as many starts (first-call costs: BLAS pool,
+    # surface upload paths, device buffers grown to the run's size)
+    DoubleHestonJumpCalibrator(S0, r, opts, N=N).calibrate(maxiter=2, multi_start=n_starts,
                                                            driver=driver)
     cal = DoubleHestonJumpCalibrator(S0, r, opts, N=N)
     if world > 1:
