@@ -549,3 +549,30 @@ def test_one_shot_price_and_loss_batch(dh, calib_golden):
     pz[3] = 0.0
     lz, _ = ctx.loss_batch(X[:1], Km, Tm, cm, pz, 100.0, 0.05, 128)
     assert np.isinf(lz[0])
+
+
+def test_edge_series_lengths_and_extreme_contracts(dh):
+    """Odd and extreme COS lengths (1 .. DH_MAX_N) on contracts far outside the golden grid's
+    range (T from 1.5 days to 10 years, K/S0 from 0.3 to 3, calls and puts), through both the
+    paired launch and the surface (fused/split) path, against the oracle's vector form.
+    Tolerance: the bar plus 1e-9 relative / 1e-9 absolute fidelity.  The oracle's own two fp64
+    forms (price_vec vs price_scalar) differ by up to 1.5e-10 absolute on this grid."""
+    from dhcos import _native
+    ctx = _native.default_context()
+    prm = np.array([0.04, 2.0, 0.04, 0.3, -0.6, 0.05, 0.8, 0.05, 0.2, -0.4, 0.1, -0.05, 0.08])
+    Ts = np.array([0.004, 0.02, 0.5, 5.0, 10.0])
+    ks = np.array([0.3, 0.7, 1.0, 1.5, 3.0])
+    T = np.repeat(Ts, 2 * ks.size)
+    K = 100.0 * np.tile(np.repeat(ks, 2), Ts.size)
+    call = np.tile([1, 0], Ts.size * ks.size).astype(np.int8)
+    rec = np.zeros((1, 16))
+    rec[0, :13], rec[0, 13], rec[0, 14] = prm, 100.0, 0.03
+    surf = _native.Surface(ctx, K, T, call)
+    for N in (1, 2, 3, 63, 65, 100, 257, 1000, _native.MAX_N):
+        want = O.price_many(prm, 100.0, K, T, 0.03, call.astype(bool), N)
+        pair = ctx.price_pairs(np.repeat(rec, K.size, axis=0), K, T, call, N)
+        tile = surf.price(rec, N=N)[0]
+        for got in (pair, tile):
+            assert np.isfinite(got).all(), N
+            assert rel_close(got, want, BAR_RTOL, BAR_ATOL).all(), (N, np.abs(got - want).max())
+            assert rel_close(got, want, 1e-9, 1e-9).all(), (N, np.abs(got - want).max())
