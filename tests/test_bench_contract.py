@@ -42,3 +42,24 @@ def test_bench_line_contract():
     c = line["cpu_baseline"]
     assert c["kind"] in ("port", "reference") and c["value"] > 0 and c["cores"] == 2
     assert c["sample"]
+
+
+@pytest.mark.gpu
+def test_bench_line_contract_two_ranks():
+    """The driver's N > 1 launch shape (torch.distributed.run, one JSON line from rank 0), rehearsed
+    with two gloo ranks sharing the box's one GPU: n_gpus = 2, weak scaling, value = both ranks'
+    prices per step / the max-over-ranks step time, no CPU-baseline leg at N > 1."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29533", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--config", "c1", "--steps", "5", "--warmup", "2", "--no-calib",
+           "--backend", "gloo"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and "cpu_baseline" not in line
+    per_step = line["config"]["prices_per_step"]
+    got = line["value"] * line["ms_per_step"] * 1e-3
+    assert abs(got - 2 * per_step) <= 1e-6 * per_step     # prices_per_step is per rank
