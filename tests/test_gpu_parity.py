@@ -576,3 +576,39 @@ def test_edge_series_lengths_and_extreme_contracts(dh):
             assert np.isfinite(got).all(), N
             assert rel_close(got, want, BAR_RTOL, BAR_ATOL).all(), (N, np.abs(got - want).max())
             assert rel_close(got, want, 1e-9, 1e-9).all(), (N, np.abs(got - want).max())
+
+
+def test_generator_batch_full_size_c5(dh):
+    """BASELINE config C5 at full size: 1M parameter sets (synthetic_generator.py ranges) x 32
+    calls (8 K/S0 in linspace(0.8, 1.2) of each sample's spot x T in {0.25, 0.5, 1, 2}), N=128,
+    in one call.  Size-independent properties: every price finite, positive and inside the
+    no-arbitrage band max(S0 - K e^{-rT}, 0) - 1e-6 S0 <= C <= S0; sampled rows equal to 1e-12
+    to the same rows priced in a small call (the large-tile kernel); and spot rows against the
+    oracle at the fidelity tolerance."""
+    from dhcos import _native
+    rs = np.random.RandomState(55)
+    P, N = 1_000_000, 128
+    Krel = np.tile(np.linspace(80.0, 120.0, 8), 4)
+    T = np.repeat([0.25, 0.5, 1.0, 2.0], 8)
+    call = np.ones(T.size, dtype=np.int8)
+    from dhcos.generator import PARAM_RANGES
+    lo, hi = np.array(list(PARAM_RANGES.values())).T
+    rec = np.zeros((P, 16))
+    rec[:, :13] = lo + (hi - lo) * rs.rand(P, 13)
+    rec[:, 13] = 100.0 * np.exp(rs.normal(0, 0.1, P))
+    rec[:, 14] = 0.03
+    ctx = _native.default_context()
+    surf = _native.Surface(ctx, Krel, T, call, strike_mode=_native.STRIKE_PCT_SPOT)
+    big = surf.price(rec, N)
+    assert big.shape == (P, T.size)
+    S = rec[:, 13:14]
+    intrinsic = np.maximum(S - (Krel / 100.0)[None, :] * S * np.exp(-0.03 * T)[None, :], 0.0)
+    assert np.isfinite(big).all() and (big > 0).all()
+    assert (big >= intrinsic - 1e-6 * S).all() and (big <= S).all()
+    rows = np.sort(rs.choice(P, 64, replace=False))
+    small = surf.price(rec[rows], N)       # other kernel, other lane split: sum order differs
+    assert rel_close(big[rows], small, 1e-12, 1e-12).all(), np.abs(big[rows] - small).max()
+    for rr in rows[:4]:
+        want = O.price_many(rec[rr, :13], rec[rr, 13], Krel * rec[rr, 13] / 100.0, T, 0.03,
+                            True, N)
+        assert rel_close(big[rr], want, FID_RTOL, BAR_ATOL).all(), (rr, big[rr] - want)
