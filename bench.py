@@ -198,29 +198,34 @@ CONFIGS = {
 }
 
 
-def calib_leg(S0, r, opts, N, n_starts, world, coll, driver):
+def calib_leg(S0, r, opts, N, n_starts, world, coll, driver, reps=3):
     """Time calibrate(maxiter=300, multi_start=n_starts) under np.random.seed(0) (starts
     sharded over the ranks at N > 1) with the given optimizer driver; max over ranks."""
     # untimed warm-up of the same driver with as many starts (first-call costs: BLAS pool,
     # surface upload paths, device buffers grown to the run's size)
     DoubleHestonJumpCalibrator(S0, r, opts, N=N).calibrate(maxiter=2, multi_start=n_starts,
                                                            driver=driver)
-    cal = DoubleHestonJumpCalibrator(S0, r, opts, N=N)
-    if world > 1:
-        dist.barrier()
-    np.random.seed(0)
-    t0 = time.perf_counter()
-    if world > 1:
-        res = calibrate_sharded(cal, maxiter=300, multi_start=n_starts, driver=driver)
-    else:
-        res = cal.calibrate(maxiter=300, multi_start=n_starts, driver=driver)
-    tc = time.perf_counter() - t0
+    # median of `reps` identical runs (each from np.random.seed(0), so the same trajectory): the
+    # SciPy driver is host-bound and a single run carries the host's scheduling noise
+    times = []
+    for _ in range(reps):
+        cal = DoubleHestonJumpCalibrator(S0, r, opts, N=N)
+        if world > 1:
+            dist.barrier()
+        np.random.seed(0)
+        t0 = time.perf_counter()
+        if world > 1:
+            res = calibrate_sharded(cal, maxiter=300, multi_start=n_starts, driver=driver)
+        else:
+            res = cal.calibrate(maxiter=300, multi_start=n_starts, driver=driver)
+        times.append(time.perf_counter() - t0)
+    tc = float(np.median(times))
     if world > 1:
         tt = torch.tensor([tc], dtype=torch.float64, device=coll)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         tc = float(tt.item())
     return {"driver": driver, "calibrations_per_sec": 1.0 / tc, "starts_per_sec": n_starts / tc,
-            "seconds": tc, "starts": n_starts, "iterations": int(res.iterations),
+            "seconds": tc, "runs": reps, "iterations": int(res.iterations), "starts": n_starts,
             "final_loss": float(res.final_loss), "message": res.message,
             "lockstep_launches_rank0": int(getattr(cal, "lockstep_launches", 0)),
             "loss_evals_rank0": int(cal.loss_evals),
