@@ -122,9 +122,12 @@ int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params
  * SciPy's 2-point forward difference (loss(x0 + h_i e_i) - f) / ((x0_i + h_i) - x0_i) with
  * h = 1e-8 (scipy/optimize/_numdiff.py:498-511,592-596), low[S] = the smallest valid loss of the
  * 14 points (best_loss, :171-172).  The 14 x S records are formed on the host and priced in one
- * request (dh_surface_loss).                                                                   */
-int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0, int S, double S0, double r,
-                  int N, double L, double* f, double* g, double* low);
+ * request (dh_surface_loss).
+ * model: [2][S][13] model params (transform_params, lbfgs_calibrator.py:62-87) of x0 (block 0)
+ * and of x0 + h (block 1, h as above), formed by the caller with the same exp / tanh the
+ * reference's NumPy uses, so f equals compute_loss(x0) bit for bit; NULL = libm exp / tanh here. */
+int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0, const double* model, int S,
+                  double S0, double r, int N, double L, double* f, double* g, double* low);
 
 /* ---- device-resident multi-start L-BFGS-B ------------------------------------------------- */
 /* Runs S independent L-BFGS-B starts (no bounds) on the surface's calibration loss without a

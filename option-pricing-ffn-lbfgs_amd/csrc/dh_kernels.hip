@@ -573,9 +573,11 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     }
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
-    if (A.partials_only) {          // plain stores: the next launch (the step kernel) reads them;
-        if (t == 0)                 // a tile with an invalid price stores NaN (the set's loss is then
-            A.part_sse[task] = f > 0.0 ? __builtin_nan("") : s;   // 1e10 whatever its sum)
+    if (A.partials_only) {          // plain stores: the next launch (the step kernel) reads them
+        if (t == 0) {
+            A.part_sse[task] = s;
+            A.part_bad[task] = (int)f;
+        }
         return;
     }
     unsigned old = 0;
@@ -846,7 +848,9 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
             double ss, cs;
             dh::dsincos(ustep * (cl ? 0.0 : xK - C.a), &ss, &cs);
             lcs[i] = cs;
-            lss[i] = cl ? NAN : ss;                                  // NaN marks clamped
+            // NaN marks clamped; a NaN sine of an unclamped option (NaN params, strike or
+            // range) is stored as 0: its NaN cosine and offset still make the price NaN
+            lss[i] = cl ? NAN : (ss == ss ? ss : 0.0);
             if (cl) record_price(A, p, lperm[i], lmkt[i], i, clp[gpos], lsse, lbad);
         }
     }
@@ -1203,7 +1207,7 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
             double ss, cs;
             dh::dsincos(ustep * (cl ? 0.0 : L.xK[i] - a), &ss, &cs);
             L.cs[i] = cs;
-            L.ss[i] = cl ? NAN : ss;
+            L.ss[i] = cl ? NAN : (ss == ss ? ss : 0.0);   // as cos_option_kernel
             if (cl) record_price(A, p, L.perm[i], L.mkt[i], i, lclp[i], L.sse, L.bad);
         }
     }
@@ -1497,10 +1501,33 @@ int spin_sync(hipStream_t st) {
     }
 }
 
-int set_device(dh_ctx* ctx) {
-    HIP_TRY(hipSetDevice(ctx->device));
-    return DH_OK;
-}
+}  // namespace
+
+// Makes the context's device current for one C-ABI call and restores the caller's device on
+// return.  The HIP runtime is shared with torch (one libamdhip64 per process), so leaving another
+// device current would move torch's current device under the caller (a rank's RCCL tensors would
+// land on the wrong GPU).
+struct DeviceScope {
+    int prev = -1;
+    int rc = DH_OK;
+    explicit DeviceScope(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev == device) return;
+        const hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) {
+            rc = fail(DH_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+            prev = -1;
+        }
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
+namespace {
 
 int ensure_attrs(dh_ctx* ctx) {
     if (ctx->attr_set) return DH_OK;
@@ -1724,8 +1751,12 @@ int dh_ctx_create(int device, dh_ctx** out) {
     dh_ctx* c = new (std::nothrow) dh_ctx();
     if (!c) return fail(DH_E_ALLOC, "ctx alloc");
     c->device = device;
-    e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    DeviceScope dev_scope(device);
+    if (dev_scope.rc) {
+        delete c;
+        return dev_scope.rc;
+    }
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
         return fail(DH_E_HIP, std::string("stream create: ") + hipGetErrorString(e));
@@ -1736,7 +1767,7 @@ int dh_ctx_create(int device, dh_ctx** out) {
 
 int dh_ctx_destroy(dh_ctx* ctx) {
     if (!ctx) return DH_OK;
-    (void)hipSetDevice(ctx->device);
+    DeviceScope dev_scope(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->params, &ctx->out, &ctx->sse, &ctx->bad, &ctx->part_sse,
                       &ctx->part_bad, &ctx->counter, &ctx->exact_prices, &ctx->stamps, &ctx->table,
@@ -1758,7 +1789,8 @@ int dh_ctx_destroy(dh_ctx* ctx) {
 
 int dh_ctx_synchronize(dh_ctx* ctx) {
     if (!ctx) return fail(DH_E_ARG, "ctx is null");
-    HIP_TRY(hipSetDevice(ctx->device));
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return DH_OK;
 }
@@ -1780,7 +1812,8 @@ int dh_ctx_read_stamps(dh_ctx* ctx, unsigned long long* out, int64_t cap, int64_
     if (!ctx || !n) return fail(DH_E_ARG, "null argument");
     *n = ctx->stamps_n;
     if (!out || ctx->stamps_n == 0) return DH_OK;
-    HIP_TRY(hipSetDevice(ctx->device));
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, ctx->stamps.ptr, (size_t)std::min<int64_t>(cap, ctx->stamps_n) * 8,
@@ -1812,8 +1845,8 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
     if (M > 0 && (!K || !T || !is_call)) return fail(DH_E_ARG, "K/T/is_call is null");
     if (strike_mode != DH_STRIKE_ABSOLUTE && strike_mode != DH_STRIKE_PCT_SPOT)
         return fail(DH_E_ARG, "bad strike_mode");
-    int rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     // group by exact maturity (stable), cut groups into tiles of <= kTileMax options
     std::vector<int> perm(M);
     std::iota(perm.begin(), perm.end(), 0);
@@ -1897,7 +1930,7 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
 
 int dh_surface_destroy(dh_surface* s) {
     if (!s) return DH_OK;
-    if (s->ctx) (void)hipSetDevice(s->ctx->device);
+    DeviceScope dev_scope(s->ctx ? s->ctx->device : 0);
     for (void* p : {(void*)s->K, (void*)s->T, (void*)s->mkt, (void*)s->call, (void*)s->perm,
                     (void*)s->tiles, (void*)s->tile_group, (void*)s->group_T, (void*)s->groups})
         if (p) (void)hipFree(p);
@@ -1946,8 +1979,8 @@ int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_param
     if (rc) return rc;
     if (P < 0) return fail(DH_E_ARG, "P < 0");
     if (P == 0 || s->M == 0) return DH_OK;
-    rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     PriceArgs A = surface_args(s, d_params, P, N, L);
     A.exact = ctx->exact;
     A.out = d_out;
@@ -1967,8 +2000,8 @@ static int surface_loss_launch(dh_ctx* ctx, const dh_surface* s, const double* d
     if (rc) return rc;
     if (S < 0) return fail(DH_E_ARG, "S < 0");
     if (S == 0) return DH_OK;
-    rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     if (s->M == 0) {
         HIP_TRY(hipMemsetAsync(d_sse, 0, (size_t)S * 8, st));
@@ -2012,8 +2045,8 @@ int dh_surface_price(dh_ctx* ctx, const dh_surface* s, const double* params, int
     if (rc) return rc;
     if (P < 0) return fail(DH_E_ARG, "P < 0");
     if (P == 0 || s->M == 0) return DH_OK;
-    rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     const size_t pb = (size_t)P * DH_PARAM_STRIDE * 8, ob = (size_t)P * s->M * 8;
     HIP_TRY(ctx->params.reserve(pb));
     HIP_TRY(ctx->out.reserve(ob));
@@ -2033,8 +2066,8 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
     if (rc) return rc;
     if (S < 0) return fail(DH_E_ARG, "S < 0");
     if (S == 0) return DH_OK;
-    rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     const size_t pb = (size_t)S * DH_PARAM_STRIDE * 8;
     double* d_prices = nullptr;
     const size_t ob = (size_t)S * s->M * 8;
@@ -2085,8 +2118,8 @@ int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const dou
     if (rc) return rc;
     if (P < 0) return fail(DH_E_ARG, "P < 0");
     if (P == 0) return DH_OK;
-    rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     const size_t pb = (size_t)P * DH_PARAM_STRIDE * 8, vb = (size_t)P * 8;
     hipStream_t st = ctx->stream;
     PriceArgs A{};
@@ -2163,8 +2196,8 @@ int dh_cf(dh_ctx* ctx, const double* params, const double* u, int n, double tau,
     if (!ctx || !params || (n > 0 && (!u || !re || !im))) return fail(DH_E_ARG, "null argument");
     if (n < 0) return fail(DH_E_ARG, "n < 0");
     if (n == 0) return DH_OK;
-    int rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     const size_t vb = (size_t)n * 8;
     HIP_TRY(ctx->params.reserve(DH_PARAM_STRIDE * 8));
     HIP_TRY(ctx->aux0.reserve(vb));
@@ -2188,8 +2221,8 @@ int dh_trunc_range(dh_ctx* ctx, const double* params, const double* K, const dou
     if (!ctx || (P > 0 && (!params || !K || !T || !a || !b))) return fail(DH_E_ARG, "null argument");
     if (P < 0) return fail(DH_E_ARG, "P < 0");
     if (P == 0) return DH_OK;
-    int rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     const size_t pb = (size_t)P * DH_PARAM_STRIDE * 8, vb = (size_t)P * 8;
     HIP_TRY(ctx->params.reserve(pb));
     HIP_TRY(ctx->aux0.reserve(vb));
@@ -2216,8 +2249,8 @@ int dh_cos_coeffs(dh_ctx* ctx, const int32_t* k, int n, double c, double d, doub
     if (!ctx || (n > 0 && (!k || !chi || !psi))) return fail(DH_E_ARG, "null argument");
     if (n < 0) return fail(DH_E_ARG, "n < 0");
     if (n == 0) return DH_OK;
-    int rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     const size_t vb = (size_t)n * 8;
     HIP_TRY(ctx->aux0.reserve((size_t)n * 4));
     HIP_TRY(ctx->aux1.reserve(vb));
@@ -2292,7 +2325,12 @@ __device__ __forceinline__ double row_min(double m) {
     return fmin(m, dpp_f64<kDppMirror>(m));
 }
 __device__ __forceinline__ double dot(WaveVec a, WaveVec b) { return row_sum(a.v * b.v); }
-__device__ __forceinline__ double amax(WaveVec a) { return fmax(0.0, row_max(fabs(a.v))); }
+// max |a_i|; a NaN component makes it NaN (SciPy's projected-gradient norm: any NaN gradient
+// component fails the pgtol test)
+__device__ __forceinline__ double amax(WaveVec a) {
+    const double m = fmax(0.0, row_max(fabs(a.v)));
+    return __any(a.v != a.v) ? __builtin_nan("") : m;
+}
 __device__ __forceinline__ bool equal(WaveVec a, WaveVec b) { return __all(a.v == b.v); }
 
 // The pair memory in LDS: s_j, y_j as 16-double rows (lane i reads column i), rho_j and the
@@ -2373,7 +2411,8 @@ struct LbArgs {
     int mode;                  // 0 begin at x0, 1 consume the request and advance, 2 re-emit
     int part_mode;             // 1: the request ran fused with partials_only -- sum its tile
                                // partials here (the hand-off's order); 0: read sse / bad
-    const double* part_sse;    // [n_live * 14][n_tiles] (part_mode 1; NaN: invalid price)
+    const double* part_sse;    // [n_live * 14][n_tiles] (part_mode 1)
+    const int* part_bad;       // [n_live * 14][n_tiles] invalid prices per tile (part_mode 1)
     int n_tiles;
     int n_inline;              // live list passed by value below (saves a dependent load), or 0
     int live_inline[kLbInline];
@@ -2435,22 +2474,28 @@ __device__ void lb_emit(const WaveCore& c, WaveVec& dx, WaveVec& pen, double* pb
 // l + 64, ... in order, then an xor butterfly), formed by one lane: leaf l as that lane's sum,
 // then the butterfly's tree (level w adds leaves w apart).  Leaves past nt are +0.0 and adding
 // +0.0 to a partial (a sum of squares) changes no bit, so W = 16 or 32 leaves give the 64-leaf
-// tree's bits.  Loads are clamped in-bounds and issued before any add.  A tile with an invalid
-// price stored NaN instead of its partial, and a NaN sum marks the set invalid (its loss is 1e10
-// whatever the sum; a valid sum is never NaN: its terms are squares, at worst +inf).
+// tree's bits.  Loads are clamped in-bounds and issued before any add.  The tiles' invalid-price
+// counts travel in their own array (pb), so a NaN sum (a NaN or infinite market price) stays the
+// NaN loss the reference gives, and an invalid price gives 1e10 whatever the sum.
 template <int W>
-__device__ __forceinline__ void lb_tile_tree(const double* ps, int nt, double& sse, int& bad) {
+__device__ __forceinline__ void lb_tile_tree(const double* ps, const int* pb, int nt, double& sse,
+                                             int& bad) {
     double x[W];
+    int nb = 0;
 #pragma unroll
     for (int u = 0; u < W; ++u) {
         const double v = ps[min(u, nt - 1)];
+        const int b = pb[min(u, nt - 1)];
         x[u] = 0.0 + (u < nt ? v : 0.0);
+        nb |= u < nt ? b : 0;
     }
     for (int j0 = W; j0 < nt; j0 += W) {          // W = 64 only
 #pragma unroll
         for (int u = 0; u < W; ++u) {
             const double v = ps[min(j0 + u, nt - 1)];
+            const int b = pb[min(j0 + u, nt - 1)];
             x[u] += j0 + u < nt ? v : 0.0;
+            nb |= j0 + u < nt ? b : 0;
         }
     }
 #pragma unroll
@@ -2459,7 +2504,7 @@ __device__ __forceinline__ void lb_tile_tree(const double* ps, int nt, double& s
         for (int u = 0; u < W; u += 2 * w) x[u] = x[u] + x[u + w];
     }
     sse = x[0];
-    bad = isnan(x[0]) ? 1 : 0;                     // a tile stored NaN: an invalid price
+    bad = nb != 0 ? 1 : 0;
 }
 
 // One wave per live start: load the state (vectors into registers, lane i = component i; the
@@ -2501,10 +2546,12 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
             const int li = lane & 15;
             if (li < dhlb::kPts) {
                 const int nt = A.n_tiles;
-                const double* ps = A.part_sse + ((size_t)slot * dhlb::kPts + li) * nt;
-                if (nt <= 16) lb_tile_tree<16>(ps, nt, req_sse, req_bad);
-                else if (nt <= 32) lb_tile_tree<32>(ps, nt, req_sse, req_bad);
-                else lb_tile_tree<64>(ps, nt, req_sse, req_bad);
+                const size_t o = ((size_t)slot * dhlb::kPts + li) * nt;
+                const double* ps = A.part_sse + o;
+                const int* pb = A.part_bad + o;
+                if (nt <= 16) lb_tile_tree<16>(ps, pb, nt, req_sse, req_bad);
+                else if (nt <= 32) lb_tile_tree<32>(ps, pb, nt, req_sse, req_bad);
+                else lb_tile_tree<64>(ps, pb, nt, req_sse, req_bad);
             }
         } else if (A.mode == 1 && (lane & 15) < dhlb::kPts) {
             const size_t i = (size_t)slot * dhlb::kPts + (lane & 15);
@@ -2621,8 +2668,8 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
         return fail(DH_E_ARG, "maxiter and maxfun must be >= 0, maxls >= 1");
     if (n_launches) *n_launches = 0;
     if (S == 0) return DH_OK;
-    rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t st = ctx->stream;
     const size_t npts = (size_t)S * dhlb::kPts;
@@ -2678,6 +2725,8 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
     A.M = s->M;
     A.mode = 0;
     A.part_mode = 0;
+    A.part_sse = nullptr;
+    A.part_bad = nullptr;
     A.n_tiles = s->n_tiles;
     auto set_inline = [&](const int* lst, int n) {
         A.n_inline = n <= kLbInline ? 1 : 0;
@@ -2713,6 +2762,7 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
             // a fused request stored its tile partials only (no hand-off): the step sums them
             A.part_mode = !ctx->exact && ctx->last_path == DH_PATH_FUSED ? 1 : 0;
             A.part_sse = (const double*)ctx->part_sse.ptr;
+            A.part_bad = (const int*)ctx->part_bad.ptr;
             e = launch_lb_step(st, A, n_live);
             if (e) return e;
             ++launches;
@@ -2799,8 +2849,8 @@ extern "C" int dh_ctx_read_lb_trace(dh_ctx* ctx, double* out, int64_t cap, int64
     if (!ctx || !n || (cap > 0 && !out)) return fail(DH_E_ARG, "null argument");
     *n = 0;
     if (ctx->lb_trace_cap == 0 || !ctx->lb_trace_n.ptr) return DH_OK;
-    int rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     unsigned long long cnt = 0;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipMemcpy(&cnt, ctx->lb_trace_n.ptr, 8, hipMemcpyDeviceToHost));
@@ -2875,8 +2925,8 @@ extern "C" int dh_loss_batch(dh_ctx* ctx, const double* x, int S, const double* 
         }
         return DH_OK;
     }
-    rc = set_device(ctx);
-    if (rc) return rc;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
     dh_surface* s = nullptr;
     rc = dh_surface_create(ctx, K, T, is_call, mkt, M, DH_STRIKE_ABSOLUTE, &s);
     if (rc) return rc;
@@ -2916,8 +2966,9 @@ extern "C" int dh_loss_batch(dh_ctx* ctx, const double* x, int S, const double* 
 // ----------------------------------------------------------------------------------------------
 // function + FD-gradient requests for the host (SciPy) driver
 // ----------------------------------------------------------------------------------------------
-extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0, int S, double S0,
-                             double r, int N, double L, double* f, double* g, double* low) {
+extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
+                             const double* model, int S, double S0, double r, int N, double L,
+                             double* f, double* g, double* low) {
     if (!ctx || !s || (S > 0 && (!x0 || !f || !g || !low))) return fail(DH_E_ARG, "null argument");
     if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
     if (s->M == 0) return fail(DH_E_ARG, "empty market (the loss is NaN)");
@@ -2929,7 +2980,10 @@ extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
     std::vector<int32_t> bad(P);
     // the request's points (scipy/optimize/_numdiff.py:498-511: x0, then x0 + h_i e_i with
     // h = 1e-8, or sqrt(eps) sign(x) max(1, |x|) where the absolute step vanishes), their model
-    // params (exp / tanh / identity, lbfgs_calibrator.py:62-87) and Feller penalties (:113-116)
+    // params (exp / tanh / identity, lbfgs_calibrator.py:62-87) and Feller penalties (:113-116).
+    // The caller passes the model params of x0 and x0 + h (model: [2][S][13]) when they must be
+    // the bits of its own exp / tanh (NumPy's, as the reference's transform_params); otherwise
+    // they come from libm here.
     for (int st = 0; st < S; ++st) {
         const double* x = x0 + (size_t)st * kN;
         double pb[kN], pp[kN];
@@ -2939,9 +2993,14 @@ extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
                 h = kSqrtEps * (x[i] >= 0.0 ? 1.0 : -1.0) * std::max(1.0, std::fabs(x[i]));
             const double xh = x[i] + h;
             dx[(size_t)st * kN + i] = xh - x[i];
-            const bool th = i == 4 || i == 9, id = i == 11;
-            pb[i] = th ? std::tanh(x[i]) : (id ? x[i] : std::exp(x[i]));
-            pp[i] = th ? std::tanh(xh) : (id ? xh : std::exp(xh));
+            if (model) {
+                pb[i] = model[(size_t)st * kN + i];
+                pp[i] = model[((size_t)S + st) * kN + i];
+            } else {
+                const bool th = i == 4 || i == 9, id = i == 11;
+                pb[i] = th ? std::tanh(x[i]) : (id ? x[i] : std::exp(x[i]));
+                pp[i] = th ? std::tanh(xh) : (id ? xh : std::exp(xh));
+            }
         }
         for (int t = 0; t < kP; ++t) {
             double* o = rec.data() + ((size_t)st * kP + t) * DH_PARAM_STRIDE;

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 import threading
 
 import numpy as np
@@ -82,7 +83,7 @@ SIGNATURES = {
                                  C.c_double, _dp]),
     "dh_loss_batch": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp, _i8p, _dp, C.c_int, C.c_double,
                                 C.c_double, C.c_int, C.c_double, _dp, _i32p]),
-    "dh_surface_fg": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_double, C.c_double, C.c_int,
+    "dh_surface_fg": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, C.c_double, C.c_double, C.c_int,
                                 C.c_double, _vp, _vp, _vp]),
     "dh_price_pairs": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
@@ -378,15 +379,22 @@ class Surface:
                                              C.byref(nl)))
         return list(res)[:S], nl.value
 
-    def fg(self, X0, S0, r, N=128, L=10.0):
-        """dh_surface_fg: (f [S], g [S, 13], low [S]) of one FD request per row of X0 [S, 13]."""
+    def fg(self, X0, S0, r, N=128, L=10.0, model=None):
+        """dh_surface_fg: (f [S], g [S, 13], low [S]) of one FD request per row of X0 [S, 13].
+        model: [2, S, 13] model params of x0 and x0 + h (dhcos.calibrator.fd_models), or None
+        for libm's exp / tanh in the library."""
         X0 = _f64(X0).reshape(-1, 13)
         S = X0.shape[0]
+        if model is not None:
+            model = _f64(model)
+            if model.shape != (2, S, 13):
+                raise ValueError(f"model must be [2, {S}, 13], got {model.shape}")
         f, g, low = np.empty(S), np.empty((S, 13)), np.empty(S)
         with self.ctx._lock:
-            _check(load().dh_surface_fg(self.ctx.handle, self._h, X0.ctypes.data, S, float(S0),
-                                        float(r), int(N), float(L), f.ctypes.data, g.ctypes.data,
-                                        low.ctypes.data))
+            _check(load().dh_surface_fg(self.ctx.handle, self._h, X0.ctypes.data,
+                                        None if model is None else model.ctypes.data, S,
+                                        float(S0), float(r), int(N), float(L), f.ctypes.data,
+                                        g.ctypes.data, low.ctypes.data))
         return f, g, low
 
     # device-pointer variants (torch tensors or raw device addresses)
@@ -425,10 +433,31 @@ def gen_draw(n_samples, lo, hi, n_opt, alpha, spot0, ret_mu, ret_sigma, noise_si
 _tls = threading.local()
 
 
+def resolve_device(device: int | None = None) -> int:
+    """The GPU a call without an explicit ``device=`` runs on, in this order: $DHCOS_DEVICE;
+    under torch.distributed (one process per GPU, e.g. torchrun) the rank's own GPU, i.e.
+    $LOCAL_RANK modulo the visible devices, else torch's current device; otherwise 0.
+    ``distributed._comm_device`` puts the collectives' tensors on the same GPU."""
+    if device is not None:
+        return int(device)
+    env = os.environ.get("DHCOS_DEVICE")
+    if env not in (None, ""):
+        return int(env)
+    torch = sys.modules.get("torch")
+    dist = getattr(torch, "distributed", None) if torch is not None else None
+    if dist is not None and dist.is_available() and dist.is_initialized():
+        local = os.environ.get("LOCAL_RANK")
+        if local not in (None, ""):
+            n = device_count()
+            return int(local) % n if n > 0 else int(local)
+        if torch.cuda.is_available():
+            return int(torch.cuda.current_device())
+    return 0
+
+
 def default_context(device: int | None = None) -> Context:
-    """Per-thread cached context on ``device`` (default: $DHCOS_DEVICE or 0)."""
-    if device is None:
-        device = int(os.environ.get("DHCOS_DEVICE", "0"))
+    """Per-thread cached context on ``device`` (default: resolve_device())."""
+    device = resolve_device(device)
     cache = getattr(_tls, "ctxs", None)
     if cache is None:
         cache = _tls.ctxs = {}
@@ -439,5 +468,5 @@ def default_context(device: int | None = None) -> Context:
 
 
 __all__ = ["gen_draw", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
-           "runtime_shared_with_torch", "PARAM_STRIDE", "MAX_N", "STRIKE_ABSOLUTE",
+           "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "STRIKE_ABSOLUTE",
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "LIB_PATH", "SIGNATURES"]

@@ -103,6 +103,29 @@ def fd_request_points(x0, h=FD_ABS_STEP):
 _SQRT_EPS = float(np.sqrt(np.finfo(np.float64).eps))
 
 
+_EXP_MASK = np.zeros(N_PARAMS, dtype=bool)
+_EXP_MASK[_EXP] = True
+
+
+def fd_models(X0, h=FD_ABS_STEP):
+    """[2, S, 13]: the model params (x_to_model) of every x0 row and of x0 + h, h as
+    fd_request_points_many forms it.  NumPy's exp / tanh as the reference's transform_params
+    calls them element by element (the same SIMD loops, so the same bits), in three ufunc calls:
+    the per-iteration host cost of the SciPy driver (tests/test_gpu_parity.py holds fg() to
+    fg_from_losses() bit for bit)."""
+    X0 = np.asarray(X0, dtype=np.float64)
+    Xh = X0 + h
+    vanish = (Xh - X0) == 0
+    if vanish.any():
+        sign = np.where(X0 >= 0, 1.0, -1.0)
+        Xh = X0 + np.where(vanish, _SQRT_EPS * sign * np.maximum(1.0, np.abs(X0)), h)
+    XX = np.concatenate([X0, Xh])
+    P = np.exp(XX, out=XX.copy(), where=_EXP_MASK)      # identity where the mask is off
+    P[:, 4] = np.tanh(XX[:, 4])
+    P[:, 9] = np.tanh(XX[:, 9])
+    return P.reshape(2, X0.shape[0], N_PARAMS)
+
+
 def fg_from_losses(cal, X0):
     """fg_batch through ``cal.loss_batch``: the 14 points of each request, their losses, SciPy's
     forward difference and the smallest valid loss (NaN never wins, 1e10 is not valid)."""
@@ -223,16 +246,16 @@ class DoubleHestonJumpCalibrator:
     def fg_batch(self, X0: np.ndarray):
         """One SciPy function+gradient request per row of X0 [S, 13] in one launch:
         -> (f [S], g [S, 13], low [S] = smallest valid loss of each request's 14 points).
-        Natively (dh_surface_fg: FD points, transforms, Feller and the gradient formed in C++
-        around one loss request) unless a subclass replaces loss_batch, whose values are then
-        used the same way."""
+        Natively (dh_surface_fg: FD points, Feller and the gradient formed in C++ around one loss
+        request; the transforms by NumPy, fd_models) unless a subclass replaces loss_batch,
+        whose values are then used the same way."""
         X0 = np.atleast_2d(np.asarray(X0, dtype=np.float64))
         native = type(self).loss_batch is DoubleHestonJumpCalibrator.loss_batch
         surf = self._get_surface() if native and len(self.market_options) else None
         if surf is None:
             return fg_from_losses(self, X0)
         self.loss_evals += X0.shape[0] * (N_PARAMS + 1)
-        return surf.fg(X0, self.spot, self.risk_free_rate, self.N)
+        return surf.fg(X0, self.spot, self.risk_free_rate, self.N, model=fd_models(X0))
 
     def compute_loss(self, x: np.ndarray) -> float:
         """Relative MSE + Feller penalty (lbfgs_calibrator.py:118-177)."""
@@ -454,6 +477,7 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
     order = [list(range(n))] if lockstep else [[s] for s in range(n)]
     with _single_threaded_blas():
         _advance(cal, gens, states, order, outcomes)
+    cal.start_stats = [(st.n_calls, st.best_loss) for st in states]
     last = states[-1]
     cal.n_calls, cal.best_loss = last.n_calls, last.best_loss   # state after the last start
     return outcomes
@@ -520,6 +544,7 @@ def run_starts_device(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int):
                              status=r.warnflag, message=msg, x=np.array(r.x[:]),
                              success=(r.warnflag == 0))
         outcomes.append((opt, t0 + r.t_done))
+    cal.start_stats = [(r.n_calls, r.best_loss) for r in res]
     cal.n_calls, cal.best_loss = res[-1].n_calls, res[-1].best_loss   # state after the last start
     cal.loss_evals += sum(r.n_calls for r in res)
     cal.lockstep_launches = launches

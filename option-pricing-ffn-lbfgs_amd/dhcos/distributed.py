@@ -8,12 +8,14 @@ is exchanged: the shards are independent and each rank drives its own GPU.
     nit, nfev, time, x[13], message bytes) gives every rank the whole table, and the best start is
     chosen exactly as the reference does -- strict ``<`` over starts in start order
     (lbfgs_calibrator.py:271-299).  Start x0s are drawn on rank 0 in start order from the global
-    ``np.random`` stream (the reference's only RNG consumer, :256) and broadcast, so the result
-    equals the single-process ``calibrate`` with the same RNG state.
+    ``np.random`` stream (the reference's only RNG consumer, :256) and broadcast with rank 0's
+    RNG state after the draws, so the result, ``n_calls`` / ``best_loss`` (those of the last
+    start) and every rank's ``np.random`` stream afterwards equal the single-process
+    ``calibrate`` with the same RNG state.
   * ``generate_sharded``: rank 0 draws every sample's random numbers in reference order
     (synthetic_generator.py:98-141) and broadcasts them; rank r prices a contiguous block of
     samples; one all-gather assembles the prices on every rank; rank 0 builds and saves the
-    reference output.
+    reference output.  Every rank's ``np.random`` ends where rank 0's draws left it.
 
 Only collectives on small host-side records and (generator) the price block are used; the COS
 kernels never wait on another rank.
@@ -31,14 +33,16 @@ from .calibrator import (CalibrationResult, DoubleHestonJumpCalibrator, N_PARAMS
                          run_starts_device)
 
 _MSG_BYTES = 64                        # SciPy messages are <= 52 characters
-_REC = 7 + N_PARAMS                    # status, start, fun, success, nit, nfev, t_rel, x[13]
+# status, start, fun, success, nit, nfev, t_rel, n_calls, best_loss, x[13]
+_REC = 9 + N_PARAMS
 _REC_I64 = _REC + _MSG_BYTES // 8
 
 
-def _comm_device(group=None):
-    """Device on which collectives of this group take tensors (RCCL: the rank's GPU)."""
+def _comm_device(group=None, device=None):
+    """Device on which collectives of this group take tensors (RCCL: the rank's GPU, the one its
+    kernels run on: _native.resolve_device)."""
     if dist.get_backend(group) == "nccl":
-        return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cuda", _native.resolve_device(device))
     return torch.device("cpu")
 
 
@@ -48,9 +52,9 @@ def _world(group=None):
     return dist.get_rank(group), dist.get_world_size(group)
 
 
-def _broadcast_f64(arr, shape, group=None):
+def _broadcast_f64(arr, shape, group=None, device=None):
     """Broadcast a float64 array from rank 0 (bit-exact)."""
-    dev = _comm_device(group)
+    dev = _comm_device(group, device)
     t = torch.empty(shape, dtype=torch.float64, device=dev)
     if dist.get_rank(group) == 0:
         t.copy_(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64).reshape(shape)))
@@ -63,11 +67,13 @@ def start_shard(n_starts: int, rank: int, world: int):
     return list(range(rank, n_starts, world))
 
 
-def _encode(s, out, t0):
-    """Fixed-size int64 record of one start's outcome (doubles bit-cast, message as bytes)."""
+def _encode(s, out, t0, stats=(0, np.inf)):
+    """Fixed-size int64 record of one start's outcome (doubles bit-cast, message as bytes).
+    stats: the start's (n_calls, best_loss), kept whether or not the start finished."""
     rec = np.zeros(_REC_I64, dtype=np.int64)
     d = np.zeros(_REC, dtype=np.float64)
     d[1] = s
+    d[7], d[8] = stats
     if out is not None:
         res, t_done = out
         d[0] = 1.0
@@ -76,7 +82,7 @@ def _encode(s, out, t0):
         d[4] = res.nit
         d[5] = res.nfev
         d[6] = t_done - t0
-        d[7:] = res.x
+        d[9:] = res.x
         msg = str(res.message).encode("utf-8")[:_MSG_BYTES]
         rec[_REC:] = np.frombuffer(msg.ljust(_MSG_BYTES, b"\0"), dtype=np.int64)
     rec[:_REC] = d.view(np.int64)
@@ -85,53 +91,81 @@ def _encode(s, out, t0):
 
 def _decode(rec):
     d = rec[:_REC].view(np.float64)
+    stats = (int(d[7]), float(d[8]))
     if d[0] != 1.0:
-        return int(d[1]), None
+        return int(d[1]), None, stats
     msg = rec[_REC:].tobytes().rstrip(b"\0").decode("utf-8", "replace")
     return int(d[1]), dict(fun=float(d[2]), success=bool(d[3]), nit=int(d[4]), nfev=int(d[5]),
-                           t_rel=float(d[6]), x=d[7:].copy(), message=msg)
+                           t_rel=float(d[6]), x=d[9:].copy(), message=msg), stats
 
 
-def gather_start_records(local, n_starts, group=None):
-    """All-gather the per-start records of every rank; returns [n_starts] decoded outcomes."""
+def gather_start_records(local, n_starts, group=None, device=None):
+    """All-gather the per-start records of every rank -> ([n_starts] decoded outcomes,
+    [n_starts] (n_calls, best_loss))."""
     rank, world = _world(group)
     n_max = (n_starts + world - 1) // world
     buf = np.zeros((n_max, _REC_I64), dtype=np.int64)
     buf[:, :_REC] = np.full(_REC, -1.0).view(np.int64)      # padding rows: start index -1
     for i, rec in enumerate(local):
         buf[i] = rec
-    dev = _comm_device(group)
+    dev = _comm_device(group, device)
     mine = torch.from_numpy(buf).to(dev)
     parts = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(parts, mine, group=group)
-    table = [None] * n_starts
+    table, stats = [None] * n_starts, [(0, np.inf)] * n_starts
     for p in parts:
         for row in p.cpu().numpy():
-            s, out = _decode(row)
+            s, out, st = _decode(row)
             if 0 <= s < n_starts:
-                table[s] = out
-    return table
+                table[s], stats[s] = out, st
+    return table, stats
+
+
+def _rng_state_vec():
+    """np.random's legacy MT19937 state as float64 (uint32 key words are exact in a double)."""
+    name, key, pos, has_gauss, cached = np.random.get_state()
+    if name != "MT19937":
+        raise ValueError(f"unsupported bit generator {name}")
+    return np.concatenate([np.asarray(key, dtype=np.float64), [pos, has_gauss, cached]])
+
+
+def _set_rng_state_vec(v):
+    key = v[:624].astype(np.uint32)
+    np.random.set_state(("MT19937", key, int(v[624]), int(v[625]), float(v[626])))
 
 
 def calibrate_sharded(cal: DoubleHestonJumpCalibrator, maxiter: int = 300, multi_start: int = 3,
-                      *, group=None, x0s=None, driver: str = "scipy") -> CalibrationResult:
-    """``cal.calibrate(maxiter, multi_start, driver=driver)`` with the starts sharded over the
-    process group.  Every rank returns the same ``CalibrationResult``."""
+                      *, group=None, x0s=None, x0=None,
+                      driver: str = "scipy") -> CalibrationResult:
+    """``cal.calibrate(maxiter, multi_start, x0s=x0s, x0=x0, driver=driver)`` with the starts
+    sharded over the process group.  Every rank returns the same ``CalibrationResult`` and ends
+    with the same ``cal.n_calls`` / ``cal.best_loss`` and ``np.random`` state."""
     rank, world = _world(group)
     if world == 1:
-        return cal.calibrate(maxiter=maxiter, multi_start=multi_start, x0s=x0s, driver=driver)
+        return cal.calibrate(maxiter=maxiter, multi_start=multi_start, x0s=x0s, x0=x0,
+                             driver=driver)
     if driver not in ("scipy", "device"):
         raise ValueError(f"driver must be 'scipy' or 'device', not {driver!r}")
     t0 = time.time()
-    if x0s is None and rank == 0:
-        x0s = [cal.get_initial_guess(guess_type=s % 3) for s in range(multi_start)]
-    x0s = _broadcast_f64(None if x0s is None else np.asarray(x0s), (multi_start, N_PARAMS),
-                         group)
+    dev = cal.device
+    block = None
+    if rank == 0:           # draws in start order (:256), then the state the draws left behind
+        if x0s is None:
+            x0s = cal.start_points(multi_start, x0)
+        block = np.concatenate([np.asarray(x0s, dtype=np.float64).reshape(-1),
+                                _rng_state_vec()])
+    block = _broadcast_f64(block, (multi_start * N_PARAMS + 627,), group, dev)
+    x0s = block[:multi_start * N_PARAMS].reshape(multi_start, N_PARAMS)
+    _set_rng_state_vec(block[multi_start * N_PARAMS:])
     mine = start_shard(multi_start, rank, world)
     run = run_starts_device if driver == "device" else run_starts
     outcomes = run(cal, [x0s[s] for s in mine], maxiter) if mine else []
-    local = [_encode(s, o, t0) for s, o in zip(mine, outcomes)]
-    table = gather_start_records(local, multi_start, group)
+    stats_local = getattr(cal, "start_stats", None) if mine else []
+    local = [_encode(s, o, t0, stats_local[i] if stats_local else (0, np.inf))
+             for i, (s, o) in enumerate(zip(mine, outcomes))]
+    table, stats = gather_start_records(local, multi_start, group, dev)
+    if multi_start > 0:     # the per-start resets (:253-254): the state after the last start
+        cal.n_calls, cal.best_loss = stats[multi_start - 1]
 
     best, best_loss = None, np.inf
     for s, out in enumerate(table):          # strict < in start order (:271)
@@ -183,11 +217,14 @@ def generate_sharded(n_samples: int = 500,
     n_opt = len(G.STRIKES_PCT) * len(G.MATURITIES)
     width = 13 + 1 + n_opt
     draws = None
-    if rank == 0:
+    if rank == 0:           # the draws, then the RNG state they leave (every rank continues there)
         params, spots, noise = G.draw_paths(n_samples)
-        draws = np.concatenate([params, spots[:, None], noise], axis=1)
+        draws = np.concatenate([np.concatenate([params, spots[:, None], noise], axis=1).ravel(),
+                                _rng_state_vec()])
     if world > 1:
-        draws = _broadcast_f64(draws, (n_samples, width), group)
+        draws = _broadcast_f64(draws, (n_samples * width + 627,), group, device)
+        _set_rng_state_vec(draws[n_samples * width:])
+    draws = draws[:n_samples * width].reshape(n_samples, width)
     params, spots, noise = draws[:, :13], draws[:, 13], draws[:, 14:]
     lo, hi = sample_block(n_samples, rank, world)
     block = price_fn(params[lo:hi], spots[lo:hi]) if hi > lo else np.empty((0, n_opt))
@@ -195,7 +232,7 @@ def generate_sharded(n_samples: int = 500,
         per = (n_samples + world - 1) // world
         buf = np.zeros((per, n_opt))
         buf[:hi - lo] = block
-        dev = _comm_device(group)
+        dev = _comm_device(group, device)
         mine = torch.from_numpy(buf).to(dev)
         parts = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(parts, mine, group=group)

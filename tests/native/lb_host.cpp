@@ -49,10 +49,14 @@ double dot(const HVec& a, const HVec& b) {
     }
     return t[0];
 }
-double amax(const HVec& a) {
+double amax(const HVec& a) {                // a NaN component makes the norm NaN (as SciPy's)
     double m = 0.0;
-    for (int i = 0; i < kLanes; ++i) m = fmax(m, fabs(a.v[i]));
-    return m;
+    bool nan = false;
+    for (int i = 0; i < kLanes; ++i) {
+        m = fmax(m, fabs(a.v[i]));
+        nan = nan || a.v[i] != a.v[i];
+    }
+    return nan ? __builtin_nan("") : m;
 }
 bool equal(const HVec& a, const HVec& b) {
     bool e = true;

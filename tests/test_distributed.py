@@ -65,19 +65,33 @@ def _free_port():
         return s.getsockname()[1]
 
 
+WARM = {"v1_0": 0.05, "kappa1": 1.8, "theta1": 0.045, "sigma1": 0.28, "rho1": -0.55,
+        "v2_0": 0.035, "kappa2": 1.2, "theta2": 0.04, "sigma2": 0.22, "rho2": -0.35,
+        "lambda_j": 0.12, "mu_j": -0.02, "sigma_j": 0.09}
+
+
 def _worker(rank, world, port, out_dir, n_starts, n_samples):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    os.environ.pop("DHCOS_DEVICE", None)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from dhcos import _native
+        dev = _native.resolve_device()          # the rank's own GPU under torch.distributed
         # only rank 0's RNG state matters: x0s and generator draws are broadcast from it
         np.random.seed(0 if rank == 0 else 1234 + rank)
         cal = OracleCalibrator(SPOT, R, _market(), N=64)
         res = D.calibrate_sharded(cal, maxiter=2, multi_start=n_starts)
+        stats = (cal.n_calls, cal.best_loss)
+        rng_after_cal = np.random.random(4)
+        cal_w = OracleCalibrator(SPOT, R, _market(), N=64)
+        res_w = D.calibrate_sharded(cal_w, maxiter=2, multi_start=n_starts, x0=WARM)
         np.random.seed(7 if rank == 0 else 99)
         gen = D.generate_sharded(n_samples, os.path.join(out_dir, f"gen{rank}.pkl"), N=64,
                                  verbose=False, price_fn=oracle_price_fn)
+        rng_after_gen = np.random.random(4)
         with open(os.path.join(out_dir, f"rank{rank}.pkl"), "wb") as fh:
-            pickle.dump({"res": res, "gen": gen}, fh)
+            pickle.dump({"res": res, "gen": gen, "stats": stats, "rng_cal": rng_after_cal,
+                         "res_w": res_w, "rng_gen": rng_after_gen, "dev": dev}, fh)
     finally:
         dist.destroy_process_group()
 
@@ -93,17 +107,27 @@ def test_sharded_equals_single_process(tmp_path, world, n_starts):
     np.random.seed(0)
     cal = OracleCalibrator(SPOT, R, _market(), N=64)
     want = cal.calibrate(maxiter=2, multi_start=n_starts)
-    for g in got:                       # every rank holds the same, reference-identical result
-        r = g["res"]
-        assert r.final_loss == want.final_loss
-        assert r.iterations == want.iterations
-        assert r.message == want.message
-        assert r.success == want.success
-        assert r.parameters == want.parameters
-        np.testing.assert_array_equal(r.model_prices, want.model_prices)
+    want_stats = (cal.n_calls, cal.best_loss)
+    want_rng = np.random.random(4)
+    want_w = OracleCalibrator(SPOT, R, _market(), N=64).calibrate(maxiter=2,
+                                                                   multi_start=n_starts, x0=WARM)
+    for rank, g in enumerate(got):      # every rank holds the same, reference-identical result
+        assert g["dev"] == rank         # LOCAL_RANK (no device here: modulo nothing)
+        for r, w in ((g["res"], want), (g["res_w"], want_w)):
+            assert r.final_loss == w.final_loss
+            assert r.iterations == w.iterations
+            assert r.message == w.message
+            assert r.success == w.success
+            assert r.parameters == w.parameters
+            np.testing.assert_array_equal(r.model_prices, w.model_prices)
+        assert g["stats"] == want_stats                     # n_calls / best_loss of the last start
+        np.testing.assert_array_equal(g["rng_cal"], want_rng)   # every rank's RNG continues alike
 
     np.random.seed(7)
     p, s, nz = G.draw_paths(n_samples)
+    want_rng_gen = np.random.random(4)
+    for g in got:
+        np.testing.assert_array_equal(g["rng_gen"], want_rng_gen)
     ref = G.assemble(p, s, nz, oracle_price_fn(p, s), None, verbose=False)
     gen = got[0]["gen"]
     assert len(gen) == n_samples
@@ -124,5 +148,14 @@ def test_shard_helpers():
     blocks = [D.sample_block(10, r, 4) for r in range(4)]
     assert blocks == [(0, 3), (3, 6), (6, 9), (9, 10)]
     assert D.sample_block(2, 3, 4) == (2, 2)
-    s, out = D._decode(D._encode(5, None, 0.0))
-    assert s == 5 and out is None
+    s, out, st = D._decode(D._encode(5, None, 0.0, (28, 0.5)))
+    assert s == 5 and out is None and st == (28, 0.5)
+
+
+def test_resolve_device(monkeypatch):
+    from dhcos import _native
+    monkeypatch.delenv("DHCOS_DEVICE", raising=False)
+    assert _native.resolve_device(3) == 3
+    assert _native.resolve_device() == 0            # no process group: device 0
+    monkeypatch.setenv("DHCOS_DEVICE", "2")
+    assert _native.resolve_device() == 2

@@ -149,9 +149,9 @@ def test_device_replays_bitwise_on_cpu_build(dh, calib_golden):
 
 def test_invalid_prices_mark_the_loss_on_both_drivers(dh, calib_golden):
     """A start whose prices are invalid (v0 = e^40 overflows the CF: NaN prices) has loss 1e10 at
-    every point (lbfgs_calibrator.py:152-158).  The device driver's loss requests store a NaN
-    partial for such a tile instead of the hand-off's bad count; both drivers must end the same
-    way: ABNORMAL at x0 with fun = 1e10 and the same request count."""
+    every point (lbfgs_calibrator.py:152-158).  The device driver's loss requests store each
+    tile's partial and its invalid-price count; both drivers must end the same way: ABNORMAL at x0
+    with fun = 1e10 and the same request count."""
     from dhcos.calibrator import run_starts, run_starts_device
     x0 = np.array(calib_golden["calibrate_seed0_starts"][0]["x0"], dtype=float)
     x0[0] = x0[5] = 40.0
@@ -160,6 +160,28 @@ def test_invalid_prices_mark_the_loss_on_both_drivers(dh, calib_golden):
     assert dev.fun == host.fun == 1e10
     assert (dev.nit, dev.nfev, dev.message) == (host.nit, host.nfev, host.message)
     assert np.array_equal(dev.x, host.x) and np.array_equal(dev.x, x0)
+
+
+def test_nan_market_price_gives_nan_loss_on_both_drivers(dh, calib_golden):
+    """A NaN (or infinite) market price makes every loss NaN in the reference (rel = NaN at that
+    option).  The device driver's loss launches carry each tile's invalid-price count apart from
+    its sum, so the NaN stays a NaN there too (not 1e10); the gradient is NaN, so the pgtol test
+    fails as in SciPy, and the line search's trial points are NaN (their prices are invalid:
+    1e10).  Both drivers end as SciPy does: ABNORMAL at x0 after 21 requests, fun = the last
+    trial's loss."""
+    from dhcos.calibrator import run_starts, run_starts_device
+    x0 = np.array(calib_golden["calibrate_seed0_starts"][1]["x0"], dtype=float)
+    for bad in (float("nan"), float("inf")):
+        mkt = [dict(o) for o in calib_golden["test_market"]]
+        mkt[4]["price"] = bad
+        cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, mkt)
+        assert np.isnan(cal.compute_loss(x0))
+        (dev, _), = run_starts_device(cal, [x0], 300)
+        (host, _), = run_starts(dh.DoubleHestonJumpCalibrator(100.0, 0.05, mkt), [x0], 300)
+        assert np.array_equal(dev.fun, host.fun, equal_nan=True)
+        assert (dev.nit, dev.nfev, dev.message) == (host.nit, host.nfev, host.message) == \
+            (0, 21, "ABNORMAL: ")
+        assert np.array_equal(dev.x, host.x) and np.array_equal(dev.x, x0)
 
 
 def test_degenerate_markets_fall_back_to_reference_semantics(dh, calib_golden):

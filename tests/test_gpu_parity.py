@@ -239,6 +239,59 @@ def test_fd_batch_one_launch(dh, calib_golden):
     assert abs(cal.compute_loss_and_grad(np.array(g["fd_guess0"]["x0"]))[1][8] - 80.0) < 0.01
 
 
+def test_fg_equals_per_point_losses_bitwise(dh, calib_golden):
+    """fg_batch (the SciPy driver's one native call per lockstep iteration: FD points, Feller
+    terms and the gradient formed in C++ around one loss request) gives the bits of compute_loss
+    at each of a request's 14 points: the model params of x and x + h come from NumPy's exp /
+    tanh (fd_models), as in the reference's transform_params.  Includes a component whose
+    absolute step vanishes (SciPy's relative-step fallback) and points with invalid prices."""
+    from dhcos.calibrator import fg_from_losses
+    g = calib_golden
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    X0 = [g["fd_guess0"]["x0"], g["fd_guess2"]["x0"]] + list(g["guesses_seed0"])
+    X0 += [e["x"] for e in g["loss_random_x"]] + [g["loss_absurd"]["x"]]
+    big = np.array(g["fd_guess2"]["x0"], dtype=float)
+    big[11] = 3e8                                   # mu_j: (x + 1e-8) - x == 0
+    X0 = np.array(X0 + [big], dtype=float)
+    f, G, low = cal.fg_batch(X0)
+    f2, G2, low2 = fg_from_losses(cal, X0)
+    assert np.array_equal(f, f2) and np.array_equal(G, G2, equal_nan=True)
+    assert np.array_equal(low, low2)
+    for i, x in enumerate(X0):
+        assert f[i] == cal.compute_loss(x)
+
+
+@pytest.mark.parametrize("path", ["fused", "split"])
+def test_nan_params_give_nan_prices_and_invalid_losses(dh, calib_golden, path):
+    """A NaN parameter (a line-search trial at a NaN x) prices every option NaN, as the reference
+    does, so its loss is 1e10 (lbfgs_calibrator.py:152): no option may be skipped as if its
+    truncation range had clamped it (the kernels mark clamped options by a NaN sine)."""
+    from dhcos import _native
+    g = calib_golden
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    surf = cal._get_surface()
+    rec = np.zeros((3, _native.PARAM_STRIDE))
+    rec[:, :13] = [0.04, 2.0, 0.04, 0.3, -0.5, 0.04, 1.5, 0.04, 0.2, -0.3, 0.1, 0.0, 0.1]
+    rec[:, 13:15] = (100.0, 0.05)
+    rec[1, 6] = np.nan                              # kappa2
+    rec[2, 11] = np.nan                             # mu_j
+    ctx = surf.ctx
+    ctx.set_path(_native.PATH_FUSED if path == "fused" else _native.PATH_SPLIT)
+    try:
+        pr = surf.price(rec)
+        sse, bad, pr2 = surf.loss_terms(rec, want_prices=True)
+    finally:
+        ctx.set_path(_native.PATH_AUTO)
+    assert np.isfinite(pr[0]).all() and np.isnan(pr[1:]).all()
+    assert np.array_equal(pr, pr2, equal_nan=True)
+    assert bad[0] == 0 and (bad[1:] == len(g["test_market"])).all()
+    x = np.array(g["guesses_seed0"][0], dtype=float)
+    x[3] = np.nan
+    assert cal.compute_loss(x) == 1e10
+    one = dh.DoubleHeston(100.0, 100.0, 1.0, 0.05, *rec[1, :13])
+    assert np.isnan(one.pricing())
+
+
 def test_reference_test_4_1_direct_minimize(dh, calib_golden):
     """tests/test_suite.py:305-321: minimize(compute_loss) without jac, 294 evals, ABNORMAL."""
     g = calib_golden["test_4_1"]

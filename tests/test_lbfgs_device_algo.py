@@ -112,6 +112,41 @@ def test_state_machine_matches_scipy(lbhost, name, fun, x0, maxiter, maxfun, xto
     assert abs(f - want.fun) <= 1e-9 * max(1.0, abs(want.fun))
 
 
+def _nan_all(x):                 # a NaN market price: every loss NaN, so every FD component
+    return float("nan"), np.full(N_PARAMS, np.nan)
+
+
+def _nan_component(x):           # one NaN gradient component beside a finite loss
+    f, g = _quad(x)
+    g[5] = np.nan
+    return f, g
+
+
+def _nan_region(x):              # NaN losses beyond x_1 > 1 (line-search trials step into it)
+    f, g = _quad(x)
+    return (float("nan") if x[1] > 1.0 else f), g
+
+
+@pytest.mark.parametrize("name,fun,x0", [
+    ("nan-objective", _nan_all, np.ones(N_PARAMS)),
+    ("nan-gradient-component", _nan_component, np.ones(N_PARAMS)),
+    ("nan-region", _nan_region, np.full(N_PARAMS, 0.9)),
+])
+def test_state_machine_nan_semantics_match_scipy(lbhost, name, fun, x0):
+    """NaN losses / gradients (a NaN or infinite market price makes every loss NaN, as in the
+    reference): SciPy's projected-gradient norm is NaN when any component is, so the pgtol test
+    fails and the line search runs (ABNORMAL after 20 trials); the state machine must agree."""
+    want = minimize(fun=fun, x0=x0, method="L-BFGS-B", jac=True,
+                    options={"maxiter": 300, "ftol": 1e-9, "gtol": 1e-6, "maxfun": _MAXFUN})
+    x, f, nit, nfev, msg, warn = run_host(lbhost, fun, x0, 300, _MAXFUN)
+    assert (nit, nfev, msg) == (want.nit, want.nfev, want.message), name
+    assert (warn == 0) == want.success
+    if want.nit == 0:
+        assert np.array_equal(x, want.x) and np.array_equal(f, want.fun, equal_nan=True)
+    else:
+        np.testing.assert_allclose(x, want.x, rtol=0, atol=1e-9)
+
+
 def test_reference_guess0_abnormal_is_bit_identical(lbhost, calib_golden):
     """Guess 0 on the reference's test market (oracle loss, N = 32 to keep it quick): the
     Feller kink makes every line-search trial fail; SciPy returns ABNORMAL after 21 requests
