@@ -114,19 +114,20 @@ __device__ __forceinline__ bool halted(const PriceArgs& A) {
 
 // In-kernel phase stamps, compiled only into the diagnostic build (make stamps): lane 0 of each
 // block of the option kernel writes s_memtime at its phase boundaries.
-constexpr int kStamps = 16;
+constexpr int kStamps = 24;
 #ifdef DH_STAMPS
-#define DH_STAMP(A, i)                                                                     \
+#define DH_STAMP_T(A, i, thr)                                                              \
     do {                                                                                   \
-        if ((A).stamps && threadIdx.x == 0) {                                              \
+        if ((A).stamps && threadIdx.x == (thr)) {                                          \
             unsigned long long _t;                                                         \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
             (A).stamps[(size_t)blockIdx.x * kStamps + (i)] = _t;                          \
         }                                                                                  \
     } while (0)
 #else
-#define DH_STAMP(A, i) do {} while (0)
+#define DH_STAMP_T(A, i, thr) do {} while (0)
 #endif
+#define DH_STAMP(A, i) DH_STAMP_T(A, i, 0)
 
 __host__ __device__ inline int tabs_per_p(const PriceArgs& A) { return A.paired ? 1 : A.n_groups; }
 __host__ __device__ inline int cl_words(const PriceArgs& A) { return (A.max_group + 63) / 64; }
@@ -389,11 +390,11 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                 }
             }
             if (has && wv == 0) {
+                // c1 is a sum of zeros and w0 has one nonzero term (lane 0's): their butterflies
+                // would change no bit
                 for (int off = 1; off < 64; off <<= 1) {
                     c0 += __shfl_xor(c0, off, 64);
-                    c1 += __shfl_xor(c1, off, 64);
                     c5 += __shfl_xor(c5, off, 64);
-                    w0 += __shfl_xor(w0, off, 64);
                 }
                 if (lane == 0) {
                     red[i][0] = c0;
@@ -491,23 +492,87 @@ __device__ __forceinline__ double option_sum(const Consts& C, bool is_call, doub
 // every kAnchor steps: a rounding error introduced n steps before an anchor is amplified by at
 // most n, so every cos/sin is within ~kAnchor^2 eps / 2 ~ 2e-13 of exact.  One (T2, T6)
 // ds_read_b128 serves all kR options.
-__device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double (&dx)[kR],
-                                             const double (&cg)[kR], const double (&sg)[kR],
+// One option per lane group (tile_r == 1): a lane's steps carry only this option's FMAs, so the
+// cos and sin halves accumulate apart (two independent chains, summed at the end) and the table
+// entries are read four steps ahead: each step's chain is one FMA deep and no LDS latency sits
+// between steps.
+__device__ __forceinline__ double angle_sum_1(int k1, int G, int N, double dx, double cg,
+                                              double sg, const double* tu, const double2* t26,
+                                              const double2* sct) {
+    double sc = 0.0, ss = 0.0;
+    const double c2 = 2.0 * cg;
+    const int last = N - 1;
+    for (int k0 = k1; k0 < N; k0 += kAnchor * G) {
+        double cx, sx;
+        dh::dsincos_t(tu[k0] * dx, sct, &sx, &cx);
+        double cp = cx * cg + sx * sg;                  // cos((k - G) th)
+        double sp = sx * cg - cx * sg;                  // sin((k - G) th)
+        const int kend = min(N, k0 + kAnchor * G);
+        int k = k0;
+        double2 t0 = t26[k], t1 = t26[min(k + G, last)], t2 = t26[min(k + 2 * G, last)],
+                t3 = t26[min(k + 3 * G, last)];
+        for (; k + 3 * G < kend; k += 4 * G) {
+            const double2 n0 = t26[min(k + 4 * G, last)], n1 = t26[min(k + 5 * G, last)],
+                          n2 = t26[min(k + 6 * G, last)], n3 = t26[min(k + 7 * G, last)];
+            sc = fma(t0.x, cx, sc);                     // step k: x_{k+G} into (cp, sp)
+            ss = fma(t0.y, sx, ss);
+            cp = fma(c2, cx, -cp);
+            sp = fma(c2, sx, -sp);
+            sc = fma(t1.x, cp, sc);                     // step k + G: x_{k+2G} into (cx, sx)
+            ss = fma(t1.y, sp, ss);
+            cx = fma(c2, cp, -cx);
+            sx = fma(c2, sp, -sx);
+            sc = fma(t2.x, cx, sc);                     // step k + 2G
+            ss = fma(t2.y, sx, ss);
+            cp = fma(c2, cx, -cp);
+            sp = fma(c2, sx, -sp);
+            sc = fma(t3.x, cp, sc);                     // step k + 3G
+            ss = fma(t3.y, sp, ss);
+            cx = fma(c2, cp, -cx);
+            sx = fma(c2, sp, -sx);
+            t0 = n0;
+            t1 = n1;
+            t2 = n2;
+            t3 = n3;
+        }
+        for (; k < kend; k += G) {                      // the last < 4 steps
+            sc = fma(t0.x, cx, sc);
+            ss = fma(t0.y, sx, ss);
+            const double nc = fma(c2, cx, -cp), ns = fma(c2, sx, -sp);
+            cp = cx;
+            sp = sx;
+            cx = nc;
+            sx = ns;
+            t0 = t1;
+            t1 = t2;
+            t2 = t3;
+        }
+    }
+    return sc + ss;
+}
+
+template <int RR>
+__device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double (&dx)[RR],
+                                             const double (&cg)[RR], const double (&sg)[RR],
                                              const double* tu, const double2* t26,
-                                             const double2* sct, double (&sum)[kR]) {
+                                             const double2* sct, double (&sum)[RR]) {
+    if constexpr (RR == 1) {
+        sum[0] = angle_sum_1(k1, G, N, dx[0], cg[0], sg[0], tu, t26, sct);
+        return;
+    }
 #pragma unroll
-    for (int j = 0; j < kR; ++j) sum[j] = 0.0;
-    double c2[kR];
+    for (int j = 0; j < RR; ++j) sum[j] = 0.0;
+    double c2[RR];
 #pragma unroll
-    for (int j = 0; j < kR; ++j) c2[j] = 2.0 * cg[j];
+    for (int j = 0; j < RR; ++j) c2[j] = 2.0 * cg[j];
     // segments of kAnchor steps, each opened by an exact (k, k - G) pair; inside a segment two
     // steps per iteration, so x_k and x_{k-G} swap registers instead of being copied, with the
     // next table entry read ahead of the arithmetic that needs it
     for (int k0 = k1; k0 < N; k0 += kAnchor * G) {
-        double cx[kR], sx[kR], cp[kR], sp[kR];
+        double cx[RR], sx[RR], cp[RR], sp[RR];
         const double uk = tu[k0];
 #pragma unroll
-        for (int j = 0; j < kR; ++j) {
+        for (int j = 0; j < RR; ++j) {
             dh::dsincos_t(uk * dx[j], sct, &sx[j], &cx[j]);
             cp[j] = cx[j] * cg[j] + sx[j] * sg[j];              // cos((k - G) th)
             sp[j] = sx[j] * cg[j] - cx[j] * sg[j];              // sin((k - G) th)
@@ -518,7 +583,7 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
         for (; k + G < kend; k += 2 * G) {
             const double2 tb = t26[k + G];
 #pragma unroll
-            for (int j = 0; j < kR; ++j) {                      // step k: x_{k+G} into (cp, sp)
+            for (int j = 0; j < RR; ++j) {                      // step k: x_{k+G} into (cp, sp)
                 sum[j] = fma(ta.x, cx[j], sum[j]);
                 sum[j] = fma(ta.y, sx[j], sum[j]);
                 cp[j] = fma(c2[j], cx[j], -cp[j]);
@@ -526,7 +591,7 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
             }
             ta = t26[min(k + 2 * G, N - 1)];
 #pragma unroll
-            for (int j = 0; j < kR; ++j) {                      // step k + G: x_{k+2G} into (cx, sx)
+            for (int j = 0; j < RR; ++j) {                      // step k + G: x_{k+2G} into (cx, sx)
                 sum[j] = fma(tb.x, cp[j], sum[j]);
                 sum[j] = fma(tb.y, sp[j], sum[j]);
                 cx[j] = fma(c2[j], cp[j], -cx[j]);
@@ -535,7 +600,7 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
         }
         if (k < kend) {
 #pragma unroll
-            for (int j = 0; j < kR; ++j) {
+            for (int j = 0; j < RR; ++j) {
                 sum[j] = fma(ta.x, cx[j], sum[j]);
                 sum[j] = fma(ta.y, sx[j], sum[j]);
             }
@@ -562,15 +627,15 @@ __device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int 
 __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t task, int nopt,
                                           int t, const double* lsse, const double* lbad) {
     DH_STAMP(A, 13);
-    double s = 0.0, f = 0.0;
-    for (int i = t; i < nopt; i += 64) {
-        s += lsse[i];
-        f += lbad[i];
+    double s = 0.0;
+    int nb = 0;                     // invalid prices: a count (0/1 flags), so a ballot suffices
+    for (int i0 = 0; i0 < nopt; i0 += 64) {
+        const int i = i0 + t;
+        if (i < nopt) s += lsse[i];
+        nb += __popcll(__ballot(i < nopt && lbad[i] != 0.0));
     }
-    for (int off = 1; off < 64; off <<= 1) {
-        s += __shfl_xor(s, off, 64);
-        f += __shfl_xor(f, off, 64);
-    }
+    for (int off = 1; off < 64; off <<= 1) s += __shfl_xor(s, off, 64);
+    const double f = nb;
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
     if (A.partials_only) {          // plain stores: the next launch (the step kernel) reads them
@@ -646,14 +711,23 @@ __device__ __forceinline__ TileLds tile_lds(double* base, int N, int cap) {
     return L;
 }
 
-// lanes per group of kR options for a tile of nopt options priced by tpt threads
-// A block-wide tile (tpt == kBlock) takes any G (its partials are reduced through LDS, e.g. G = 10
-// for 100-option tiles: 250 of 256 lanes busy instead of 200 with G = 8); narrower tiles keep a
-// power of two <= 64 for the in-wave butterfly.
+// Options per lane group of a launch whose largest tile has max_nopt options priced by tpt
+// threads: kR (one table read serves kR options) unless that tile leaves >= 8 lanes per option,
+// where one option per group gives each lane one anchor sincos instead of kR and a butterfly over
+// one sum instead of kR (the latency path of small calibration tiles: C2's 32-option tiles, C1's
+// 5).  A property of the surface and N, never of the batch: every path and batch composition
+// prices a tile with the same lanes.  The request kernels are instantiated per value.
+inline int tile_r(int max_nopt, int tpt) { return tpt >= 8 * std::max(max_nopt, 1) ? 1 : kR; }
+
+// lanes per group of RT options for a tile of nopt options priced by tpt threads
+// A block-wide tile (tpt == kBlock) with kR options per group takes any G (its partials are
+// reduced through LDS, e.g. G = 10 for 100-option tiles: 250 of 256 lanes busy instead of 200 with
+// G = 8); other tiles keep a power of two <= 64 for the in-wave butterfly.
+template <int RT>
 __device__ __forceinline__ int group_lanes(int nopt, int N, int tpt) {
-    const int R = min(kR, max(nopt, 1));
+    const int R = min(RT, max(nopt, 1));
     const int ngroups = (nopt + R - 1) / R;
-    if (tpt == kBlock) return max(1, min(tpt / ngroups, N - 1));
+    if (tpt == kBlock && RT == kR) return max(1, min(tpt / ngroups, N - 1));
     int G = 1;
     while (G * 2 <= tpt / max(ngroups, 1) && G < 64) G *= 2;
     while (G > 1 && G / 2 >= N - 1) G /= 2;                 // no more lanes than terms k >= 1
@@ -665,12 +739,13 @@ __device__ __forceinline__ int group_lanes(int nopt, int N, int tpt) {
 // A block-wide tile (tpt == kBlock; every thread of the block must call this) whose G is not a
 // power of two <= 64 reduces each group's G lane partials through LDS (red: kR x kBlock doubles)
 // in lane order; otherwise xor butterflies inside the wave.
-__device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const Consts& C,
-                                          double S0, double disc, int nopt, int G, int tpt, int t,
-                                          bool active, const TileLds& L, double* red,
-                                          const double2* sct) {
+template <int RT>
+__device__ __forceinline__ void tile_sums_r(const PriceArgs& A, int64_t p, const Consts& C,
+                                            double S0, double disc, int nopt, int G, int tpt,
+                                            int t, bool active, const TileLds& L, double* red,
+                                            const double2* sct) {
     const int N = A.N;
-    const int R = min(kR, max(nopt, 1));
+    const int R = min(RT, max(nopt, 1));
     const int ngroups = (nopt + R - 1) / R;
     const int groups_per_pass = max(1, tpt / G);
     const bool lds_red = tpt == kBlock && (G > 64 || (G & (G - 1)) != 0);   // else butterflies
@@ -678,10 +753,10 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
         const int gi = pass + t / G;
         const int gl = t % G;
         const bool gvalid = active && t < groups_per_pass * G && gi < ngroups;
-        double dx[kR], cs[kR], ss[kR];
-        bool use[kR];
+        double dx[RT], cs[RT], ss[RT];
+        bool use[RT];
 #pragma unroll
-        for (int j = 0; j < kR; ++j) {
+        for (int j = 0; j < RT; ++j) {
             const int oi = gi * R + j;
             const bool in = gvalid && j < R && oi < nopt;
             const double sj = in ? L.ss[oi] : 0.0;
@@ -690,14 +765,14 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
             cs[j] = use[j] ? L.cs[oi] : 1.0;
             ss[j] = use[j] ? sj : 0.0;
         }
-        double sm[kR];
+        double sm[RT];
         if (pass == 0) DH_STAMP(A, 9);
-        angle_sums_r(1 + gl, G, N, dx, cs, ss, L.tu, L.t26, sct, sm);
+        angle_sums_r<RT>(1 + gl, G, N, dx, cs, ss, L.tu, L.t26, sct, sm);
         if (pass == 0) DH_STAMP(A, 10);
         if (lds_red) {
             if (gvalid) {
 #pragma unroll
-                for (int j = 0; j < kR; ++j) red[j * kBlock + t] = sm[j];
+                for (int j = 0; j < RT; ++j) red[j * kBlock + t] = sm[j];
             }
             __syncthreads();
             if (pass == 0) DH_STAMP(A, 11);
@@ -719,7 +794,7 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
         }
         for (int off = 1; off < G; off <<= 1) {
 #pragma unroll
-            for (int j = 0; j < kR; ++j) sm[j] += __shfl_xor(sm[j], off, 64);
+            for (int j = 0; j < RT; ++j) sm[j] += __shfl_xor(sm[j], off, 64);
         }
         if (pass == 0) DH_STAMP(A, 11);
         // every lane of the group holds the (bitwise identical) sums: lane j finalises option j
@@ -727,7 +802,7 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
             double m = sm[0];
             bool mu = use[0];
 #pragma unroll
-            for (int j = 1; j < kR; ++j) {
+            for (int j = 1; j < RT; ++j) {
                 m = gl == j ? sm[j] : m;
                 mu = gl == j ? use[j] : mu;
             }
@@ -739,7 +814,7 @@ __device__ __forceinline__ void tile_sums(const PriceArgs& A, int64_t p, const C
             }
         } else if (gl == 0) {
 #pragma unroll
-            for (int j = 0; j < kR; ++j) {
+            for (int j = 0; j < RT; ++j) {
                 if (!use[j]) continue;
                 const int oi = gi * R + j;
                 const double sum = option_sum(C, L.call[oi] != 0, S0, L.K[oi], L.xK[oi],
@@ -756,7 +831,7 @@ constexpr int kRedDoubles = kR * kBlock;
 // ----------------------------------------------------------------------------------------------
 // option kernel
 // ----------------------------------------------------------------------------------------------
-template <int TPT>
+template <int TPT, int RT>
 __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(PriceArgs A) {
     if (halted(A)) return;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -804,7 +879,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
         }
     }
     // lanes: groups of kR options on G lanes each
-    const int G = group_lanes(nopt, N, TPT);
+    const int G = group_lanes<RT>(nopt, N, TPT);
 
     const int64_t q = (p - A.p0) * tabs_per_p(A) + g;
     const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
@@ -857,7 +932,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     __syncthreads();
     DH_STAMP(A, 1);
 
-    tile_sums(A, p, C, P.S0, disc, nopt, G, TPT, t, active, L, red, sct);
+    tile_sums_r<RT>(A, p, C, P.S0, disc, nopt, G, TPT, t, active, L, red, sct);
     DH_STAMP(A, 2);
 
     // ---- loss: fixed-order per-task partial, last arriver finalises the param set ----
@@ -1067,7 +1142,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
 // the same order and with the same lane partition as cos_table_kernel<TPT1> followed by
 // cos_option_kernel<tpt2>, so the two paths give the same bits.
 // ----------------------------------------------------------------------------------------------
-template <int TPT1>
+template <int TPT1, int RT>
 __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(PriceArgs A, int tpt2) {
     // the halt test waits on a global load: taken after the staging barrier, so the load
     // overlaps the prologue instead of delaying it (a halted launch wastes the prologue only)
@@ -1135,6 +1210,9 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
             double* cc = (double*)&CC;
             for (int j = 0; j < 16; ++j) cc[j] = shc[6 + j];
         }
+        DH_STAMP(A, 6);
+        DH_STAMP_T(A, 19, 64);
+        DH_STAMP_T(A, 20, 192);
         table_entries<TPT1>(CC, t, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
             L.tu[k] = u;
             if (k == 0) {
@@ -1145,6 +1223,10 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
             const double T2 = w * S0 * dh::drcp(1.0 + u * u);
             L.t26[k] = make_double2(T2, -(T2 * dh::drcp(u)));
         });
+        DH_STAMP(A, 7);
+        DH_STAMP_T(A, 16, 64);
+        DH_STAMP_T(A, 17, 128);
+        DH_STAMP_T(A, 18, 192);
     }
     // ---- clamp-widened options (double_heston.py:135-137), decided and priced per wave ----
     for (int base = wv * 64; base < gn; base += nthr) {
@@ -1174,10 +1256,12 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
     __syncthreads();
     DH_STAMP(A, 2);
 
-    // ---- k-sums in the canonical order of a 64-thread table slot (wave 0, from the LDS table;
-    //      the same bits as cos_table_kernel) || per-option rotations ----
+    // ---- k-sums in the canonical order of a 64-thread table slot (from the LDS table; the same
+    //      bits as cos_table_kernel).  c1 is a sum of zeros (+0.0) and w0 has one nonzero term
+    //      (lane 0's), so their butterflies change no bit and are skipped || per-option
+    //      rotations ----
     if (wv == 0) {
-        double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = lane == 0 ? w0s : 0.0;
+        double c0 = 0.0, c5 = 0.0;
         for (int k = lane; k < N; k += 64) {
             if (k == 0) continue;
             const double T2 = L.t26[k].x;
@@ -1187,19 +1271,17 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
         }
         for (int off = 1; off < 64; off <<= 1) {
             c0 += __shfl_xor(c0, off, 64);
-            c1 += __shfl_xor(c1, off, 64);
             c5 += __shfl_xor(c5, off, 64);
-            w0 += __shfl_xor(w0, off, 64);
         }
         if (lane == 0) {
             red[0][0] = c0;
-            red[1][0] = c1;
+            red[1][0] = 0.0;
             red[2][0] = c5;
-            red[3][0] = w0;
+            red[3][0] = w0s;
         }
     }
-    const double disc = exp(-prm[14] * T);
-    const int G = group_lanes(gn, N, tpt2);
+    const double disc = exp(-shc[23] * T);          // r staged by the prologue: no global load
+    const int G = group_lanes<RT>(gn, N, tpt2);
     {
         const double ustep = G * dh::kPi / (b - a);
         for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {          // wave 0 does the sums
@@ -1215,7 +1297,7 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
     DH_STAMP(A, 3);
 
     const Consts C{0.0 + red[0][0], 0.0 + red[1][0], 0.0 + red[2][0], 0.0 + red[3][0], a, b, eb, ea};
-    if (t < tpt2) tile_sums(A, p, C, S0, disc, gn, G, tpt2, t, true, L, lclp + cap, sct);
+    if (t < tpt2) tile_sums_r<RT>(A, p, C, S0, disc, gn, G, tpt2, t, true, L, lclp + cap, sct);
     DH_STAMP(A, 4);
     if (A.part_sse) {
         __syncthreads();
@@ -1531,14 +1613,13 @@ namespace {
 
 int ensure_attrs(dh_ctx* ctx) {
     if (ctx->attr_set) return DH_OK;
-    HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<64>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
-    HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<128>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
-    HIP_TRY(hipFuncSetAttribute((const void*)cos_option_kernel<256>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
-    for (const void* f : {(const void*)cos_fused_kernel<64>, (const void*)cos_fused_kernel<128>,
-                          (const void*)cos_fused_kernel<256>})
+    for (const void* f :
+         {(const void*)cos_option_kernel<64, 1>, (const void*)cos_option_kernel<128, 1>,
+          (const void*)cos_option_kernel<256, 1>, (const void*)cos_option_kernel<64, kR>,
+          (const void*)cos_option_kernel<128, kR>, (const void*)cos_option_kernel<256, kR>,
+          (const void*)cos_fused_kernel<64, 1>, (const void*)cos_fused_kernel<128, 1>,
+          (const void*)cos_fused_kernel<256, 1>, (const void*)cos_fused_kernel<64, kR>,
+          (const void*)cos_fused_kernel<128, kR>, (const void*)cos_fused_kernel<256, kR>})
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
@@ -1611,10 +1692,14 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         A.stamps = (unsigned long long*)ctx->stamps.ptr;
     }
     const dim3 grid((unsigned)blocks), block((unsigned)std::max(t1, t2));
-    switch (t1) {
-        case 64: hipLaunchKernelGGL(cos_fused_kernel<64>, grid, block, lds, st, A, t2); break;
-        case 128: hipLaunchKernelGGL(cos_fused_kernel<128>, grid, block, lds, st, A, t2); break;
-        default: hipLaunchKernelGGL(cos_fused_kernel<256>, grid, block, lds, st, A, t2); break;
+    const bool r1 = tile_r(max_nopt, t2) == 1;
+    switch (t1 * (r1 ? 1 : -1)) {
+        case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1>), grid, block, lds, st, A, t2); break;
+        case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1>), grid, block, lds, st, A, t2); break;
+        case 256: hipLaunchKernelGGL((cos_fused_kernel<256, 1>), grid, block, lds, st, A, t2); break;
+        case -64: hipLaunchKernelGGL((cos_fused_kernel<64, kR>), grid, block, lds, st, A, t2); break;
+        case -128: hipLaunchKernelGGL((cos_fused_kernel<128, kR>), grid, block, lds, st, A, t2); break;
+        default: hipLaunchKernelGGL((cos_fused_kernel<256, kR>), grid, block, lds, st, A, t2); break;
     }
     HIP_TRY(hipGetLastError());
     return DH_OK;
@@ -1705,10 +1790,16 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         HIP_TRY(hipGetLastError());
         if (small) {
             hipLaunchKernelGGL(cos_option_small_kernel, dim3((unsigned)b2), dim3(kBlock), 0, st, A, L);
-        } else switch (t2) {
-            case 64: hipLaunchKernelGGL(cos_option_kernel<64>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;
-            case 128: hipLaunchKernelGGL(cos_option_kernel<128>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;
-            default: hipLaunchKernelGGL(cos_option_kernel<256>, dim3((unsigned)b2), dim3(kBlock), lds2, st, A); break;
+        } else {
+            const dim3 g2((unsigned)b2), bk(kBlock);
+            switch (t2 * (tile_r(max_nopt, t2) == 1 ? 1 : -1)) {
+                case 64: hipLaunchKernelGGL((cos_option_kernel<64, 1>), g2, bk, lds2, st, A); break;
+                case 128: hipLaunchKernelGGL((cos_option_kernel<128, 1>), g2, bk, lds2, st, A); break;
+                case 256: hipLaunchKernelGGL((cos_option_kernel<256, 1>), g2, bk, lds2, st, A); break;
+                case -64: hipLaunchKernelGGL((cos_option_kernel<64, kR>), g2, bk, lds2, st, A); break;
+                case -128: hipLaunchKernelGGL((cos_option_kernel<128, kR>), g2, bk, lds2, st, A); break;
+                default: hipLaunchKernelGGL((cos_option_kernel<256, kR>), g2, bk, lds2, st, A); break;
+            }
         }
         HIP_TRY(hipGetLastError());
     }

@@ -26,6 +26,7 @@ MAX_N = 2048
 STRIKE_ABSOLUTE = 0
 STRIKE_PCT_SPOT = 1
 PATH_AUTO, PATH_SPLIT, PATH_FUSED = 0, 1, 2
+STAMPS_PER_BLOCK = 24          # kStamps of the DH_STAMPS build (csrc/dh_kernels.hip)
 
 _dp = C.POINTER(C.c_double)
 _i8p = C.POINTER(C.c_int8)
@@ -195,7 +196,7 @@ class Context:
         if n.value:
             _check(load().dh_ctx_read_stamps(self._h, out.ctypes.data_as(C.POINTER(C.c_ulonglong)),
                                              n.value, C.byref(n)))
-        return out.reshape(-1, 16)
+        return out.reshape(-1, STAMPS_PER_BLOCK)
 
     def set_lb_trace(self, cap: int):
         """Diagnostics: record up to cap consumed requests of the next calibrate_lbfgs calls."""

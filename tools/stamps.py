@@ -72,7 +72,12 @@ def main():
                   f"max {c.max():8.0f} cycles")
         life = st[:, 5] - st[:, 0]
         print(f"  lifetime median {np.median(life):8.0f}  max {life.max():8.0f}")
-        detail = [("prologue (thread 0)", 0, 8), ("staging wait", 8, 1), ("sums: setup", 3, 9),
+        detail = [("prologue (thread 0)", 0, 8), ("staging wait", 8, 1),
+                  ("cf: consts load", 1, 6), ("cf: entries", 6, 7), ("cf: clamp+barrier", 7, 2),
+                  ("cf: start w1 - w0", 6, 19), ("cf: start w3 - w0", 6, 20),
+                  ("cf: end w1 - w0", 7, 16), ("cf: end w2 - w0", 7, 17),
+                  ("cf: end w3 - w0", 7, 18),
+                  ("sums: setup", 3, 9),
                   ("sums: angle loop", 9, 10), ("sums: butterfly", 10, 11),
                   ("sums: finalise", 11, 4), ("loss: barrier", 4, 13), ("loss: wave sums", 13, 14),
                   ("loss: store drain", 14, 15), ("loss: ticket", 15, 12), ("loss: last", 12, 5)]
