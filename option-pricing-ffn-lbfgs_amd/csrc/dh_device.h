@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "dh_logatan_table.h"
 #include "dh_sincos_table.h"
 
 namespace dh {
@@ -292,6 +293,67 @@ __device__ __forceinline__ double datan2(double y, double x) {
     return (isnan(x) || isnan(y)) ? x + y : a;
 }
 
+// ---- table-driven log and atan2 of the CF loop ----------------------------------------------
+// The CF's math tables in one LDS array of double2 (load_math_tables): [0, 128) sin / cos of
+// j pi/64 (dsincos_t), [128, 256) (invc, logc) of dlog_t, [256, 321) atan(j/64) (hi, lo) of
+// datan2_t.
+constexpr int kTabLog = 128;
+constexpr int kTabAtan = 256;
+constexpr int kMathTab = 321;
+
+// log(x) for normal x > 0 (glibc's table layout, tools/gen_logatan_tables.py): x = 2^k z with z
+// in [0.6875, 1.375) from the bits, subinterval i by the next 7 bits, r = z invc_i - 1 (one FMA,
+// |r| < 2^-8), log x = k ln2 + logc_i + log1p(r) with log1p by its Taylor series through r^7
+// (remainder < 2^-67).  Absolute error ~1 ulp of the result's scale (no special path near 1,
+// where only absolute accuracy matters here).  ~20 VALU against dlog's ~40.
+__device__ __forceinline__ double dlog_t(double x, const double2* __restrict__ tab) {
+    const long long ix = __double_as_longlong(x);
+    const long long tmp = ix - 0x3fe6000000000000LL;
+    const int i = (int)((tmp >> 45) & 127);
+    const double kd = (double)(int)(tmp >> 52);
+    const double z = __longlong_as_double(ix - (tmp & (0xfffLL << 52)));
+    const double2 e = tab[kTabLog + i];                              // (invc, logc)
+    const double r = fma(z, e.x, -1.0);
+    const double w = fma(kd, 0x1.62e42fefa3800p-1, e.y);             // k ln2_hi exact (|k| < 2^11)
+    const double hi = w + r;
+    const double lo = fma(kd, 0x1.ef35793c76730p-45, (w - hi) + r);  // k ln2_lo
+    double p = fma(r, 0.14285714285714285, -0.16666666666666666);
+    p = fma_k(r, p, 0.2);
+    p = fma_k(r, p, -0.25);
+    p = fma_k(r, p, 0.3333333333333333);
+    p = fma_k(r, p, -0.5);
+    const double y = fma(r * r, p, lo) + hi;
+    // positive normal x only (v_cmp_class: class bit 8 = +normal); anything else -- 0, inf, NaN,
+    // negative or subnormal, none of which |Q|^2 reaches for finite parameters -- gives NaN, so
+    // an out-of-range input surfaces as an invalid price instead of a wrong finite value
+    return __builtin_amdgcn_class(x, 1 << 8) ? y : NAN;
+}
+
+// atan2(y, x) in (-pi, pi], as datan2 but with the polynomial's range cut to |t'| <= 2^-7 by a
+// table: t = min/max(|x|, |y|) in [0, 1] (the v_rcp_f64 seed is enough to pick j = rint(64 t)),
+// then atan t = atan(j/64) + atan(t') with t' = (mn - mx s)/(mx + mn s), s = j/64 exact, both
+// FMAs; atan t' to t'^7.  Same quadrant rules and zero / NaN behaviour as datan2.  ~40 VALU
+// against ~50.
+__device__ __forceinline__ double datan2_t(double y, double x, const double2* __restrict__ tab) {
+    const double ax = fabs(x), ay = fabs(y);
+    const double mx = fmax(ax, ay), mn = fmin(ax, ay);
+    const double t0 = mn * __builtin_amdgcn_rcp(fmax(mx, 2.2250738585072014e-308));
+    const int j = (int)rint(t0 * 64.0);                              // 0 .. 64
+    const double sj = (double)j * 0.015625;
+    const double xp = fma(mn, sj, mx), yp = fma(-mx, sj, mn);
+    const double tp = yp * drcp(fmax(xp, 2.2250738585072014e-308));
+    const double z = tp * tp;
+    double q = fma(z, -0.14285714285714285, 0.2);
+    q = fma_k(z, q, -0.3333333333333333);
+    const double at = fma(tp * z, q, tp);
+    const double2 e = tab[kTabAtan + j];                             // atan(j/64) hi, lo
+    double a = e.x + (at + e.y);
+    a = (ay > ax) ? (1.57079632679489655800e+00 - a) + 6.12323399573676588613e-17 : a;
+    a = signbit(x) ? (3.14159265358979311600e+00 - a) + 1.22464679914735317720e-16 : a;
+    a = copysign(a, y);
+    return (isnan(x) || isnan(y)) ? x + y : a;
+}
+
 // z1 / z2 through one reciprocal of |z2|^2 (no Smith scaling: |z2| on this path stays far
 // from the fp64 over/underflow thresholds).
 __device__ __forceinline__ cplx cdiv_rcp(cplx a, cplx b) {
@@ -382,7 +444,7 @@ __device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau,
     const cplx dd = {fma(beta.re, beta.re, -beta.im * beta.im) + s2u * u,
                      2.0 * beta.re * beta.im + s2u};
     // principal sqrt: |dd|, then sqrt((|dd| + |Re|)/2) and its reciprocal (no division)
-    double h, rh, sq, rs;
+    double h, rh, sq, rs;                            // h = |dd| = |d|^2, rh = 1/|dd|
     dsqrt_rsqrt_pos(fma(dd.re, dd.re, dd.im * dd.im), h, rh);
     dsqrt_rsqrt_pos(0.5 * (h + fabs(dd.re)), sq, rs);
     const double other = 0.5 * dd.im * rs;
@@ -398,11 +460,12 @@ __device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau,
     const cplx ome = {1.0 - e.re, -e.im};
     const cplx num = cmul(cscale(bm, F.inv_s2), cmul(ome, bp));
     const cplx B = cdiv_rcp(num, D);
-    const cplx Q = cdiv_rcp(D, {2.0 * dre, 2.0 * dim});
-    const double lq_re = 0.5 * dlog(fma(Q.re, Q.re, Q.im * Q.im));
-    const double lq_im = datan2(Q.im, Q.re);
-    return {F.coef * (bm.re * tau - 2.0 * lq_re) + B.re * F.v0,
-            F.coef * (bm.im * tau - 2.0 * lq_im) + B.im * F.v0};
+    // log Q, Q = D / (2d), without the division: |Q|^2 = |D|^2 / (4 |dd|) (|d|^2 = |dd|, and 1/|dd|
+    // came with the first square root), arg Q = arg(D conj(d)) (a positive real factor apart)
+    const double lq2 = dlog_t(fma(D.re, D.re, D.im * D.im) * (0.25 * rh), sct);   // log |Q|^2
+    const double aq = datan2_t(fma(D.im, dre, -(D.re * dim)), fma(D.re, dre, D.im * dim), sct);
+    return {F.coef * (bm.re * tau - lq2) + B.re * F.v0,
+            F.coef * (bm.im * tau - 2.0 * aq) + B.im * F.v0};
 }
 
 // Per-(param set, T) constants of the fast CF.
@@ -455,10 +518,15 @@ __device__ __forceinline__ double cf_phase_re(const CfConsts& C, double u, doubl
     return cf_phase_from(C, u, a, X1, X2, jump_x(C, u, sct), sct);
 }
 
-// Block-wide copy of the sin/cos table into LDS (the caller synchronises before use).
+// Block-wide copy of the CF's math tables (kMathTab double2: sin/cos, log, atan) into LDS (the
+// caller synchronises before use).
 __device__ __forceinline__ void load_sincos_table(double2* sct) {
-    for (int i = threadIdx.x; i < 128; i += blockDim.x)
-        sct[i] = make_double2(kSinCosPi64[2 * i], kSinCosPi64[2 * i + 1]);
+    for (int i = threadIdx.x; i < kMathTab; i += blockDim.x) {
+        const double* src = i < kTabLog ? kSinCosPi64 + 2 * i
+                          : (i < kTabAtan ? kLogInvcLogc + 2 * (i - kTabLog)
+                                          : kAtanJ64 + 2 * (i - kTabAtan));
+        sct[i] = make_double2(src[0], src[1]);
+    }
 }
 
 // First two cumulants of one factor (double_heston.py:101-118).  Q1: c1 includes r*tau.

@@ -58,7 +58,7 @@ constexpr int kR = 4;             // options carried per lane in the option kern
 constexpr int kConsts = 8;        // c0, c1, c5, w0, a, b, e^b, e^a per table
 constexpr size_t kTableBudget = size_t(256) << 20;   // table workspace per chunk (MALL-sized)
 constexpr int kLdsMax = 160 * 1024;
-constexpr int kLdsDyn = kLdsMax - 4096;   // dynamic LDS cap: the kernels keep <= 4 KB static
+constexpr int kLdsDyn = kLdsMax - 8192;   // dynamic LDS cap: the kernels keep <= 8 KB static
 
 // Arrival counters of the loss hand-off, one per 128-byte line: every tile of a param set bumps
 // its set's counter with an agent-scope atomic, and packed counters put all the sets of a
@@ -279,13 +279,13 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, int64_t 
 }
 
 #ifndef DH_TABLE_WAVES
-#define DH_TABLE_WAVES 2    // min waves per SIMD: caps VGPR+AGPR at 256 (the CF needs ~250)
+#define DH_TABLE_WAVES 3    // min waves per SIMD: caps VGPR+AGPR at 168 (3 waves per SIMD)
 #endif
 #ifndef DH_OPTION_WAVES
 #define DH_OPTION_WAVES 1
 #endif
 #ifndef DH_FUSED_WAVES
-#define DH_FUSED_WAVES 2
+#define DH_FUSED_WAVES 4    // caps VGPR+AGPR at 128 (4 waves per SIMD)
 #endif
 
 // CF entries of one table slot (thread t of TPT): k = t, t + TPT, ..., emitted in increasing k
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
     __shared__ double shc[kBatch][kTabC];
     __shared__ double red[kBatch][4];
     __shared__ double w0s[kTabs];
-    __shared__ double2 sct[128];
+    __shared__ double2 sct[dh::kMathTab];
     dh::load_sincos_table(sct);           // synchronised by the first batch's barrier
     const int slot = __builtin_amdgcn_readfirstlane(threadIdx.x / TPT);
     const int t = threadIdx.x % TPT;
@@ -851,7 +851,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     const int cap = A.opt_cap;
     const TileLds L = tile_lds(smem + (size_t)slot * option_lds_doubles(N, cap), N, cap);
     double* red = smem + (size_t)kTasks * option_lds_doubles(N, cap);   // TPT == kBlock only
-    __shared__ double2 sct[128];
+    __shared__ double2 sct[dh::kMathTab];
     dh::load_sincos_table(sct);                                // synchronised by the staging barrier
     double2* t26 = L.t26;
     double* tu = L.tu;
@@ -1150,7 +1150,7 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ double shc[kTabC];
     __shared__ double red[4][1];
-    __shared__ double2 sct[128];
+    __shared__ double2 sct[dh::kMathTab];
     __shared__ unsigned long long cmask[kTileMax / 64];
     const int nthr = blockDim.x;
     const int t = threadIdx.x;

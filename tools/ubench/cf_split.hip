@@ -8,7 +8,7 @@
 __global__ void cf_one(const double* prm, double* out, long long* cyc, int reps) {
     const dh::Params P = dh::load_params(prm);
     const dh::CfConsts C = dh::cf_consts(P, 1.0);
-    __shared__ double2 sct[128];
+    __shared__ double2 sct[dh::kMathTab];
     dh::load_sincos_table(sct);
     __syncthreads();
     double u = 1.0 + (threadIdx.x & 63) * 1e-2;
@@ -31,7 +31,7 @@ __device__ __forceinline__ double shfl_xor1(double v) {
 __global__ void cf_pair(const double* prm, double* out, long long* cyc, int reps) {
     const dh::Params P = dh::load_params(prm);
     const dh::CfConsts C = dh::cf_consts(P, 1.0);
-    __shared__ double2 sct[128];
+    __shared__ double2 sct[dh::kMathTab];
     dh::load_sincos_table(sct);
     __syncthreads();
     const bool odd = threadIdx.x & 1;

@@ -46,7 +46,7 @@ __global__ void lat(double* out, long long* cyc, double seed) {
 __global__ void cf_lat(const double* prm, double* out, long long* cyc, int ilp) {
     const dh::Params P = dh::load_params(prm);
     const dh::CfConsts C = dh::cf_consts(P, 1.0);
-    __shared__ double2 sct[128];
+    __shared__ double2 sct[dh::kMathTab];
     dh::load_sincos_table(sct);
     __syncthreads();
     double u = 1.0 + threadIdx.x * 1e-3, u2 = 2.0 + threadIdx.x * 1e-3;
