@@ -518,16 +518,19 @@ __device__ __forceinline__ double cf_phase_re(const CfConsts& C, double u, doubl
     return cf_phase_from(C, u, a, X1, X2, jump_x(C, u, sct), sct);
 }
 
-// Block-wide copy of the CF's math tables (kMathTab double2: sin/cos, log, atan) into LDS (the
-// caller synchronises before use).
-__device__ __forceinline__ void load_sincos_table(double2* sct) {
-    for (int i = threadIdx.x; i < kMathTab; i += blockDim.x) {
+// Copy of the CF's math tables (kMathTab double2: sin/cos, log, atan) into LDS by the block's
+// threads from t_first on (the caller synchronises before use).
+__device__ __forceinline__ void load_math_tables(double2* sct, int t_first) {
+    for (int i = (int)threadIdx.x - t_first; i < kMathTab; i += (int)blockDim.x - t_first) {
+        if (i < 0) break;
         const double* src = i < kTabLog ? kSinCosPi64 + 2 * i
                           : (i < kTabAtan ? kLogInvcLogc + 2 * (i - kTabLog)
                                           : kAtanJ64 + 2 * (i - kTabAtan));
         sct[i] = make_double2(src[0], src[1]);
     }
 }
+
+__device__ __forceinline__ void load_sincos_table(double2* sct) { load_math_tables(sct, 0); }
 
 // First two cumulants of one factor (double_heston.py:101-118).  Q1: c1 includes r*tau.
 __device__ __forceinline__ void factor_cumulants(double tau, double r, double v0, double lm,

@@ -1181,7 +1181,7 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
     //      indices) ----
     if (wv == 0) table_prologue_wave(A, q, shc, lane);
     DH_STAMP(A, 8);
-    dh::load_sincos_table(sct);
+    dh::load_math_tables(sct, nthr > 64 ? 64 : 0);      // the waves after the prologue's
     for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
         const int m = g0 + i;
         const double K = option_strike(A, m, S0);
@@ -1228,7 +1228,22 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
         DH_STAMP_T(A, 17, 128);
         DH_STAMP_T(A, 18, 192);
     }
-    // ---- clamp-widened options (double_heston.py:135-137), decided and priced per wave ----
+    // ---- clamp-widened options (double_heston.py:135-137), decided and priced per wave: the
+    //      masks first (a short loop), the pricing loop only where a mask is set (rare: its
+    //      register traffic stays off the common path) ----
+    bool any_cl = false;
+    for (int base = wv * 64; base < gn; base += nthr) {
+        const int o = base + lane;
+        bool cl = false;
+        if (o < gn) {
+            const double xK = L.xK[o];
+            cl = xK - 0.1 < a || xK + 0.1 > b;
+        }
+        const unsigned long long mask = __ballot(cl);
+        if (lane == 0) cmask[base / 64] = mask;
+        any_cl = any_cl || mask != 0;
+    }
+    if (__builtin_expect(any_cl, 0))
     for (int base = wv * 64; base < gn; base += nthr) {
         const int o = base + lane;
         bool cl = false;
@@ -1237,7 +1252,6 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
             cl = xK - 0.1 < a || xK + 0.1 > b;
         }
         unsigned long long mask = __ballot(cl);
-        if (lane == 0) cmask[base / 64] = mask;
         if (mask == 0) continue;
         const Params P = dh::load_params(prm);
         const double disc = exp(-P.r * T);
@@ -1253,6 +1267,8 @@ __global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(Price
             if (lane == 0) lclp[base + l] = disc * v;
         }
     }
+    DH_STAMP(A, 21);
+    DH_STAMP_T(A, 22, 64);
     __syncthreads();
     DH_STAMP(A, 2);
 

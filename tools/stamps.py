@@ -76,7 +76,8 @@ def main():
                   ("cf: consts load", 1, 6), ("cf: entries", 6, 7), ("cf: clamp+barrier", 7, 2),
                   ("cf: start w1 - w0", 6, 19), ("cf: start w3 - w0", 6, 20),
                   ("cf: end w1 - w0", 7, 16), ("cf: end w2 - w0", 7, 17),
-                  ("cf: end w3 - w0", 7, 18),
+                  ("cf: end w3 - w0", 7, 18), ("cf: clamp loop w0", 7, 21),
+                  ("cf: w1 at barrier - w0 CF end", 7, 22),
                   ("sums: setup", 3, 9),
                   ("sums: angle loop", 9, 10), ("sums: butterfly", 10, 11),
                   ("sums: finalise", 11, 4), ("loss: barrier", 4, 13), ("loss: wave sums", 13, 14),
