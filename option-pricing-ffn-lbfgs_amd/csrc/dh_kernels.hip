@@ -944,21 +944,24 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
 }
 
 // ----------------------------------------------------------------------------------------------
-// option kernel, small tiles (<= kSmallTile options per tile): one lane carries kRs options of a
+// option kernel, small tiles (<= kSmallTile options per tile): one lane carries RS options of a
 // tile through every term k = 1 .. N-1.  Its step rotation e^{i th} is also its start angle, the
 // 8-byte table w_k is read straight from L2/MALL and expanded to (T2, T6) on the fly
-// (amortised over kRs options), and a task's partial is reduced over its L lanes (L = lanes per
+// (amortised over RS options), and a task's partial is reduced over its L lanes (L = lanes per
 // task, a power of two <= 4) before the same fence-free hand-off.  Per lane this is ~9 VALU
 // instructions per option-term with no LDS, no per-lane anchors and no butterflies -- the
 // large-tile kernel's fixed costs dominate when a tile has 5-16 options (generator grids).
 // ----------------------------------------------------------------------------------------------
 constexpr int kSmallTile = 16;
-constexpr int kRs = 4;
+// options per lane: 4, or 8 for tiles of more than 4 options (C5's 8-option tiles: one lane per
+// tile, so the per-term expansion of w_k is not repeated on a second lane: -24% VALU per tile-term)
+constexpr int small_rs(int max_nopt) { return max_nopt > 4 ? 8 : 4; }
 // ...and only when a call has enough tasks to fill the chip with one lane group per task
 // (below this the large-tile kernel's many lanes per option win on latency).  Calibration
 // launches (14 x starts param sets) stay far below it, so lockstep == sequential bit for bit.
 constexpr int64_t kSmallMinTasks = 65536;
 
+template <int RS>
 __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, int L) {
     if (halted(A)) return;
     const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -999,12 +1002,12 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
 
     // per option: log-strike, clamp bit; cos/sin(k th) by the Chebyshev recurrence from
     // (k = 0, k = 1) = (1 + 0i, e^{i th})
-    double dx[kRs], c[kRs], sn[kRs], cp[kRs], sp[kRs], cs[kRs], ss[kRs], sm[kRs];
-    bool use[kRs];
+    double dx[RS], c[RS], sn[RS], cp[RS], sp[RS], cs[RS], ss[RS], sm[RS];
+    bool use[RS];
     double lsum = 0.0, lbad = 0.0;
 #pragma unroll
-    for (int j = 0; j < kRs; ++j) {
-        const int oi = sub * kRs + j;
+    for (int j = 0; j < RS; ++j) {
+        const int oi = sub * RS + j;
         const bool in = active && oi < nopt;
         bool cl = false;
         double xK = 0.0;
@@ -1039,9 +1042,9 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
         sm[j] = 0.0;
     }
     const double* tw = A.table + q * (int64_t)A.N;
-    double c2[kRs];
+    double c2[RS];
 #pragma unroll
-    for (int j = 0; j < kRs; ++j) c2[j] = 2.0 * cs[j];
+    for (int j = 0; j < RS; ++j) c2[j] = 2.0 * cs[j];
     // segments of kAnchor terms (the first starts exact at k = 1; later ones re-anchor on an
     // exact (k, k - 1) pair), two terms per iteration with x_k / x_{k-1} swapping registers
     const int N = A.N;
@@ -1049,7 +1052,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
         if (k0 > 1) {
             const double uk = k0 * piba;
 #pragma unroll
-            for (int j = 0; j < kRs; ++j) {
+            for (int j = 0; j < RS; ++j) {
                 dh::dsincos(uk * dx[j], &sn[j], &c[j]);
                 cp[j] = c[j] * cs[j] + sn[j] * ss[j];
                 sp[j] = sn[j] * cs[j] - c[j] * ss[j];
@@ -1067,7 +1070,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
             const double T6b = -(T2b * dh::drcp(ub));
             wa = active ? tw[min(k + 2, N - 1)] : 0.0;
 #pragma unroll
-            for (int j = 0; j < kRs; ++j) {
+            for (int j = 0; j < RS; ++j) {
                 sm[j] = fma(T2a, c[j], sm[j]);
                 sm[j] = fma(T6a, sn[j], sm[j]);
                 cp[j] = fma(c2[j], c[j], -cp[j]);               // x_{k+1}
@@ -1083,7 +1086,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
             const double T2 = wa * S0 * dh::drcp(1.0 + u * u);
             const double T6 = -(T2 * dh::drcp(u));
 #pragma unroll
-            for (int j = 0; j < kRs; ++j) {
+            for (int j = 0; j < RS; ++j) {
                 sm[j] = fma(T2, c[j], sm[j]);
                 sm[j] = fma(T6, sn[j], sm[j]);
             }
@@ -1091,9 +1094,9 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
     }
     // finalise this lane's options, then the task partial over its L lanes (fixed tree)
 #pragma unroll
-    for (int j = 0; j < kRs; ++j) {
+    for (int j = 0; j < RS; ++j) {
         if (!use[j]) continue;
-        const int m = opt0 + sub * kRs + j;
+        const int m = opt0 + sub * RS + j;
         const double K = option_strike(A, m, S0);
         double ratio;
         const double xK = option_logk(K, S0, ratio);
@@ -1766,8 +1769,9 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     // small tiles in a large call take the lane-per-option-group kernel (decided once per call,
     // so every chunk of it runs the same arithmetic)
     const bool small = max_nopt <= kSmallTile && A0.P * tasks_per_p >= kSmallMinTasks;
+    const int rs = small_rs(max_nopt);
     int L = 1;
-    while (L * kRs < max_nopt) L *= 2;
+    while (L * rs < max_nopt) L *= 2;
     const int t2 = small ? kBlock : option_tpt(max_nopt, N, A0.opt_cap);
     const size_t lds2 =
         small ? 0 : ((size_t)(kBlock / t2) * option_lds_doubles(N, A0.opt_cap) +
@@ -1805,7 +1809,10 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         }
         HIP_TRY(hipGetLastError());
         if (small) {
-            hipLaunchKernelGGL(cos_option_small_kernel, dim3((unsigned)b2), dim3(kBlock), 0, st, A, L);
+            if (rs == 8)
+                hipLaunchKernelGGL((cos_option_small_kernel<8>), dim3((unsigned)b2), dim3(kBlock), 0, st, A, L);
+            else
+                hipLaunchKernelGGL((cos_option_small_kernel<4>), dim3((unsigned)b2), dim3(kBlock), 0, st, A, L);
         } else {
             const dim3 g2((unsigned)b2), bk(kBlock);
             switch (t2 * (tile_r(max_nopt, t2) == 1 ? 1 : -1)) {
