@@ -638,11 +638,10 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     const double f = nb;
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
-    if (A.partials_only) {          // plain stores: the next launch (the step kernel) reads them
-        if (t == 0) {
-            A.part_sse[task] = s;
-            A.part_bad[task] = (int)f;
-        }
+    if (A.partials_only) {          // plain stores: the next launch (the step kernel) reads them;
+        // the tile's invalid flag rides in the sign bit (a valid partial is a sum of squares: +0,
+        // positive, +inf or NaN, canonicalised to + here), so the step kernel reads one array
+        if (t == 0) A.part_sse[task] = f > 0.0 ? -fabs(s) : fabs(s);
         return;
     }
     unsigned old = 0;
@@ -2525,8 +2524,7 @@ struct LbArgs {
     int mode;                  // 0 begin at x0, 1 consume the request and advance, 2 re-emit
     int part_mode;             // 1: the request ran fused with partials_only -- sum its tile
                                // partials here (the hand-off's order); 0: read sse / bad
-    const double* part_sse;    // [n_live * 14][n_tiles] (part_mode 1)
-    const int* part_bad;       // [n_live * 14][n_tiles] invalid prices per tile (part_mode 1)
+    const double* part_sse;    // [n_live * 14][n_tiles] (part_mode 1; sign bit: invalid price)
     int n_tiles;
     int n_inline;              // live list passed by value below (saves a dependent load), or 0
     int live_inline[kLbInline];
@@ -2588,28 +2586,26 @@ __device__ void lb_emit(const WaveCore& c, WaveVec& dx, WaveVec& pen, double* pb
 // l + 64, ... in order, then an xor butterfly), formed by one lane: leaf l as that lane's sum,
 // then the butterfly's tree (level w adds leaves w apart).  Leaves past nt are +0.0 and adding
 // +0.0 to a partial (a sum of squares) changes no bit, so W = 16 or 32 leaves give the 64-leaf
-// tree's bits.  Loads are clamped in-bounds and issued before any add.  The tiles' invalid-price
-// counts travel in their own array (pb), so a NaN sum (a NaN or infinite market price) stays the
-// NaN loss the reference gives, and an invalid price gives 1e10 whatever the sum.
+// tree's bits.  Loads are clamped in-bounds and issued before any add.  A tile with an invalid
+// price stored its partial with the sign bit set (task_loss), so the magnitudes give the sum --
+// a NaN sum (a NaN or infinite market price) stays the NaN loss the reference gives -- and any
+// sign bit gives 1e10 whatever the sum.
 template <int W>
-__device__ __forceinline__ void lb_tile_tree(const double* ps, const int* pb, int nt, double& sse,
-                                             int& bad) {
+__device__ __forceinline__ void lb_tile_tree(const double* ps, int nt, double& sse, int& bad) {
     double x[W];
-    int nb = 0;
+    bool nb = false;
 #pragma unroll
     for (int u = 0; u < W; ++u) {
         const double v = ps[min(u, nt - 1)];
-        const int b = pb[min(u, nt - 1)];
-        x[u] = 0.0 + (u < nt ? v : 0.0);
-        nb |= u < nt ? b : 0;
+        x[u] = 0.0 + (u < nt ? fabs(v) : 0.0);
+        nb = nb || (u < nt && signbit(v));
     }
     for (int j0 = W; j0 < nt; j0 += W) {          // W = 64 only
 #pragma unroll
         for (int u = 0; u < W; ++u) {
             const double v = ps[min(j0 + u, nt - 1)];
-            const int b = pb[min(j0 + u, nt - 1)];
-            x[u] += j0 + u < nt ? v : 0.0;
-            nb |= j0 + u < nt ? b : 0;
+            x[u] += j0 + u < nt ? fabs(v) : 0.0;
+            nb = nb || (j0 + u < nt && signbit(v));
         }
     }
 #pragma unroll
@@ -2618,7 +2614,7 @@ __device__ __forceinline__ void lb_tile_tree(const double* ps, const int* pb, in
         for (int u = 0; u < W; u += 2 * w) x[u] = x[u] + x[u + w];
     }
     sse = x[0];
-    bad = nb != 0 ? 1 : 0;
+    bad = nb ? 1 : 0;
 }
 
 // One wave per live start: load the state (vectors into registers, lane i = component i; the
@@ -2660,12 +2656,10 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
             const int li = lane & 15;
             if (li < dhlb::kPts) {
                 const int nt = A.n_tiles;
-                const size_t o = ((size_t)slot * dhlb::kPts + li) * nt;
-                const double* ps = A.part_sse + o;
-                const int* pb = A.part_bad + o;
-                if (nt <= 16) lb_tile_tree<16>(ps, pb, nt, req_sse, req_bad);
-                else if (nt <= 32) lb_tile_tree<32>(ps, pb, nt, req_sse, req_bad);
-                else lb_tile_tree<64>(ps, pb, nt, req_sse, req_bad);
+                const double* ps = A.part_sse + ((size_t)slot * dhlb::kPts + li) * nt;
+                if (nt <= 16) lb_tile_tree<16>(ps, nt, req_sse, req_bad);
+                else if (nt <= 32) lb_tile_tree<32>(ps, nt, req_sse, req_bad);
+                else lb_tile_tree<64>(ps, nt, req_sse, req_bad);
             }
         } else if (A.mode == 1 && (lane & 15) < dhlb::kPts) {
             const size_t i = (size_t)slot * dhlb::kPts + (lane & 15);
@@ -2840,7 +2834,6 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
     A.mode = 0;
     A.part_mode = 0;
     A.part_sse = nullptr;
-    A.part_bad = nullptr;
     A.n_tiles = s->n_tiles;
     auto set_inline = [&](const int* lst, int n) {
         A.n_inline = n <= kLbInline ? 1 : 0;
@@ -2876,7 +2869,6 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
             // a fused request stored its tile partials only (no hand-off): the step sums them
             A.part_mode = !ctx->exact && ctx->last_path == DH_PATH_FUSED ? 1 : 0;
             A.part_sse = (const double*)ctx->part_sse.ptr;
-            A.part_bad = (const int*)ctx->part_bad.ptr;
             e = launch_lb_step(st, A, n_live);
             if (e) return e;
             ++launches;
