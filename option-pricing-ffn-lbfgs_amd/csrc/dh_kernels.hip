@@ -492,6 +492,11 @@ __device__ __forceinline__ double option_sum(const Consts& C, bool is_call, doub
 // every kAnchor steps: a rounding error introduced n steps before an anchor is amplified by at
 // most n, so every cos/sin is within ~kAnchor^2 eps / 2 ~ 2e-13 of exact.  One (T2, T6)
 // ds_read_b128 serves all kR options.
+// Table reads run ahead of the arithmetic through a per-lane pointer and are not clamped to the
+// table: an entry read past the end is never used, and an LDS read cannot fault (past the
+// workgroup's allocation it returns 0), so each read is one ds_read_b128 at an immediate or
+// uniform offset with no index arithmetic.
+//
 // One option per lane group (tile_r == 1): a lane's steps carry only this option's FMAs, so the
 // cos and sin halves accumulate apart (two independent chains, summed at the end) and the table
 // entries are read four steps ahead: each step's chain is one FMA deep and no LDS latency sits
@@ -501,7 +506,6 @@ __device__ __forceinline__ double angle_sum_1(int k1, int G, int N, double dx, d
                                               const double2* sct) {
     double sc = 0.0, ss = 0.0;
     const double c2 = 2.0 * cg;
-    const int last = N - 1;
     for (int k0 = k1; k0 < N; k0 += kAnchor * G) {
         double cx, sx;
         dh::dsincos_t(tu[k0] * dx, sct, &sx, &cx);
@@ -509,11 +513,11 @@ __device__ __forceinline__ double angle_sum_1(int k1, int G, int N, double dx, d
         double sp = sx * cg - cx * sg;                  // sin((k - G) th)
         const int kend = min(N, k0 + kAnchor * G);
         int k = k0;
-        double2 t0 = t26[k], t1 = t26[min(k + G, last)], t2 = t26[min(k + 2 * G, last)],
-                t3 = t26[min(k + 3 * G, last)];
+        const double2* tq = t26 + k;
+        double2 t0 = tq[0], t1 = tq[G], t2 = tq[2 * G], t3 = tq[3 * G];
         for (; k + 3 * G < kend; k += 4 * G) {
-            const double2 n0 = t26[min(k + 4 * G, last)], n1 = t26[min(k + 5 * G, last)],
-                          n2 = t26[min(k + 6 * G, last)], n3 = t26[min(k + 7 * G, last)];
+            tq += 4 * G;
+            const double2 n0 = tq[0], n1 = tq[G], n2 = tq[2 * G], n3 = tq[3 * G];
             sc = fma(t0.x, cx, sc);                     // step k: x_{k+G} into (cp, sp)
             ss = fma(t0.y, sx, ss);
             cp = fma(c2, cx, -cp);
@@ -565,9 +569,9 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
     double c2[RR];
 #pragma unroll
     for (int j = 0; j < RR; ++j) c2[j] = 2.0 * cg[j];
-    // segments of kAnchor steps, each opened by an exact (k, k - G) pair; inside a segment two
-    // steps per iteration, so x_k and x_{k-G} swap registers instead of being copied, with the
-    // next table entry read ahead of the arithmetic that needs it
+    // segments of kAnchor steps, each opened by an exact (k, k - G) pair; inside a segment four
+    // steps per iteration (then at most one pair and one single step), so x_k and x_{k-G} swap
+    // registers instead of being copied, with the table entries read ahead of the arithmetic
     for (int k0 = k1; k0 < N; k0 += kAnchor * G) {
         double cx[RR], sx[RR], cp[RR], sp[RR];
         const double uk = tu[k0];
@@ -579,24 +583,33 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
         }
         const int kend = min(N, k0 + kAnchor * G);
         int k = k0;
-        double2 ta = t26[k];
-        for (; k + G < kend; k += 2 * G) {
-            const double2 tb = t26[k + G];
+        const double2* tq = t26 + k;
+        double2 ta = tq[0], tb = tq[G];
+        auto step = [&](const double2& t, double (&x)[RR], double (&y)[RR], double (&xp)[RR],
+                        double (&yp)[RR]) {         // x_{k+G} into (xp, yp)
 #pragma unroll
-            for (int j = 0; j < RR; ++j) {                      // step k: x_{k+G} into (cp, sp)
-                sum[j] = fma(ta.x, cx[j], sum[j]);
-                sum[j] = fma(ta.y, sx[j], sum[j]);
-                cp[j] = fma(c2[j], cx[j], -cp[j]);
-                sp[j] = fma(c2[j], sx[j], -sp[j]);
+            for (int j = 0; j < RR; ++j) {
+                sum[j] = fma(t.x, x[j], sum[j]);
+                sum[j] = fma(t.y, y[j], sum[j]);
+                xp[j] = fma(c2[j], x[j], -xp[j]);
+                yp[j] = fma(c2[j], y[j], -yp[j]);
             }
-            ta = t26[min(k + 2 * G, N - 1)];
-#pragma unroll
-            for (int j = 0; j < RR; ++j) {                      // step k + G: x_{k+2G} into (cx, sx)
-                sum[j] = fma(tb.x, cp[j], sum[j]);
-                sum[j] = fma(tb.y, sp[j], sum[j]);
-                cx[j] = fma(c2[j], cp[j], -cx[j]);
-                sx[j] = fma(c2[j], sp[j], -sx[j]);
-            }
+        };
+        for (; k + 3 * G < kend; k += 4 * G) {
+            const double2 tc = tq[2 * G], td = tq[3 * G];
+            tq += 4 * G;
+            step(ta, cx, sx, cp, sp);
+            step(tb, cp, sp, cx, sx);
+            ta = tq[0];
+            tb = tq[G];
+            step(tc, cx, sx, cp, sp);
+            step(td, cp, sp, cx, sx);
+        }
+        if (k + G < kend) {
+            step(ta, cx, sx, cp, sp);
+            step(tb, cp, sp, cx, sx);
+            k += 2 * G;
+            ta = tq[2 * G];
         }
         if (k < kend) {
 #pragma unroll
