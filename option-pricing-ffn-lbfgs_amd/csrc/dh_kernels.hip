@@ -36,10 +36,12 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "dh_device.h"
@@ -647,7 +649,10 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
         if (i < nopt) s += lsse[i];
         nb += __popcll(__ballot(i < nopt && lbad[i] != 0.0));
     }
-    for (int off = 1; off < 64; off <<= 1) s += __shfl_xor(s, off, 64);
+    // lanes >= nopt hold +0.0 and only lane 0's sum is used, so levels with off >= nopt would add
+    // +0.0 to it (an exact no-op on a sum of squares): skip them (C2's 32 options: 5 levels)
+    const int lvl = nopt < 64 ? nopt : 64;
+    for (int off = 1; off < lvl; off <<= 1) s += __shfl_xor(s, off, 64);
     const double f = nb;
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
@@ -2542,6 +2547,16 @@ struct LbArgs {
     int n_inline;              // live list passed by value below (saves a dependent load), or 0
     int live_inline[kLbInline];
 };
+static_assert(std::is_standard_layout<LbArgs>::value, "lb_live_inline reads LbArgs by offset");
+
+// live_inline[slot] as a scalar load straight from the kernel-argument segment (LbArgs is the
+// kernel's only argument); indexing the by-value argument compiled to a flat load
+__device__ __forceinline__ int lb_live_inline(int slot) {
+    typedef const __attribute__((address_space(4))) char* KargPtr;
+    const KargPtr k = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    return ((const __attribute__((address_space(4))) int*)(k + offsetof(LbArgs, live_inline)))
+        [slot < kLbInline ? slot : 0];
+}
 
 __device__ __forceinline__ WaveVec lb_ld(const LbSlot* g, int v, int lane) {
     return {g->vec[v][lane & 15]};
@@ -2606,19 +2621,21 @@ __device__ void lb_emit(const WaveCore& c, WaveVec& dx, WaveVec& pen, double* pb
 template <int W>
 __device__ __forceinline__ void lb_tile_tree(const double* ps, int nt, double& sse, int& bad) {
     double x[W];
-    bool nb = false;
+    unsigned hi = 0;        // OR of the high words: loads past nt repeat tile nt - 1 (clamped), so
+                            // the OR over all of them is the OR of the first nt sign bits (a
+                            // short-circuit || compiled to an exec-mask branch per tile)
 #pragma unroll
     for (int u = 0; u < W; ++u) {
         const double v = ps[min(u, nt - 1)];
         x[u] = 0.0 + (u < nt ? fabs(v) : 0.0);
-        nb = nb || (u < nt && signbit(v));
+        hi |= (unsigned)__double2hiint(v);
     }
     for (int j0 = W; j0 < nt; j0 += W) {          // W = 64 only
 #pragma unroll
         for (int u = 0; u < W; ++u) {
             const double v = ps[min(j0 + u, nt - 1)];
             x[u] += j0 + u < nt ? fabs(v) : 0.0;
-            nb = nb || (j0 + u < nt && signbit(v));
+            hi |= (unsigned)__double2hiint(v);
         }
     }
 #pragma unroll
@@ -2627,7 +2644,7 @@ __device__ __forceinline__ void lb_tile_tree(const double* ps, int nt, double& s
         for (int u = 0; u < W; u += 2 * w) x[u] = x[u] + x[u + w];
     }
     sse = x[0];
-    bad = nb ? 1 : 0;
+    bad = (int)(hi >> 31);
 }
 
 // One wave per live start: load the state (vectors into registers, lane i = component i; the
@@ -2641,7 +2658,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     [[maybe_unused]] const unsigned long long t_start = lb_clock();
     const int slot = blockIdx.x;
     const int lane = threadIdx.x;
-    const int sidx = A.n_inline ? A.live_inline[slot] : A.live[slot];
+    const int sidx = A.n_inline ? lb_live_inline(slot) : A.live[slot];
     LbSlot* G = A.states + sidx;
     WaveCore c;
     [[maybe_unused]] unsigned long long t_load = 0, t_req = 0, t_sm = 0;
@@ -2665,7 +2682,10 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
         // loss terms, the pair memory, the vectors and the scalars
         if (A.mode == 1 && A.part_mode) {
             // the loss hand-off's sum (task_loss), formed by lane t of every row for point t
-            // (lb_tile_tree: the same additions, so the same bits)
+            // (lb_tile_tree: the same additions, so the same bits).  Measured alternatives, all
+            // slower: staging the request's contiguous partials through LDS with coalesced loads
+            // (C2 step load phase 4.4k -> 5.5k cycles); issuing these loads together with the
+            // state's (5.6k)
             const int li = lane & 15;
             if (li < dhlb::kPts) {
                 const int nt = A.n_tiles;
@@ -2747,7 +2767,14 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     if (need) lb_emit(c, dx, pen, pb, pp, A, slot, lane);
     __syncthreads();
     [[maybe_unused]] const unsigned long long t_emit = lb_clock();
-    for (int i = lane; i < kLbRing; i += 64) G->ring[i] = ring[i];
+    {   // every LDS read before the first store (one LDS round trip, not one per store)
+        double rg[(kLbRing + 63) / 64];
+#pragma unroll
+        for (int j = 0; j < (kLbRing + 63) / 64; ++j) rg[j] = ring[min(lane + 64 * j, kLbRing - 1)];
+#pragma unroll
+        for (int j = 0; j < (kLbRing + 63) / 64; ++j)
+            if (lane + 64 * j < kLbRing) G->ring[lane + 64 * j] = rg[j];
+    }
     lb_st(G, 0, lane, c.x);
     lb_st(G, 1, lane, c.g);
     lb_st(G, 2, lane, c.z);

@@ -34,14 +34,19 @@ def main():
     res, launches = surf.calibrate_lbfgs(x0s, S0, r, cfg["N"])
     tr = surf.ctx.read_lb_trace()
     surf.ctx.set_lb_trace(0)
-    st = tr[:, 32:38]
-    st = st[st[:, 0] > 0]
+    keep = tr[:, 32] > 0
+    sub = tr[keep][:, [32, 31, 38, 39, 33]]       # start, sidx, loads issued, loads landed, t_load
+    st = tr[keep][:, 32:38]
     print(f"{args.config} {args.starts} starts: {len(st)} consumed requests, {launches} iterations")
     names = ["load state", "consume request", "state machine", "emit request", "store state"]
     for i, nm in enumerate(names):
         c = st[:, i + 1] - st[:, i]
         print(f"  {nm:16s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}  "
               f"max {c.max():8.0f} cycles")
+    if (sub[:, 1:4] > 0).all():
+        for i, nm in enumerate(["  kernargs/sidx", "  issue loads", "  loads landed", "  tile sums"]):
+            c = sub[:, i + 1] - sub[:, i]
+            print(f"  {nm:16s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}")
     life = st[:, 5] - st[:, 0]
     print(f"  lifetime median {np.median(life):8.0f}  max {life.max():8.0f}")
 
