@@ -332,16 +332,17 @@ __device__ __forceinline__ double dlog_t(double x, const double2* __restrict__ t
 // atan2(y, x) in (-pi, pi], as datan2 but with the polynomial's range cut to |t'| <= 2^-7 by a
 // table: t = min/max(|x|, |y|) in [0, 1] (the v_rcp_f64 seed is enough to pick j = rint(64 t)),
 // then atan t = atan(j/64) + atan(t') with t' = (mn - mx s)/(mx + mn s), s = j/64 exact, both
-// FMAs; atan t' to t'^7.  Same quadrant rules and zero / NaN behaviour as datan2.  ~40 VALU
-// against ~50.
+// FMAs; atan t' to t'^7.  Same quadrant rules as datan2.  For the CF only: x, y finite and not
+// both 0 (D conj(d)), no NaN handling -- a NaN D makes log|Q|^2 NaN (dlog_t), and so the price.
+// ~35 VALU against datan2's ~50.
 __device__ __forceinline__ double datan2_t(double y, double x, const double2* __restrict__ tab) {
     const double ax = fabs(x), ay = fabs(y);
     const double mx = fmax(ax, ay), mn = fmin(ax, ay);
-    const double t0 = mn * __builtin_amdgcn_rcp(fmax(mx, 2.2250738585072014e-308));
+    const double t0 = mn * __builtin_amdgcn_rcp(mx);
     const int j = (int)rint(t0 * 64.0);                              // 0 .. 64
     const double sj = (double)j * 0.015625;
     const double xp = fma(mn, sj, mx), yp = fma(-mx, sj, mn);
-    const double tp = yp * drcp(fmax(xp, 2.2250738585072014e-308));
+    const double tp = yp * drcp(xp);
     const double z = tp * tp;
     double q = fma(z, -0.14285714285714285, 0.2);
     q = fma_k(z, q, -0.3333333333333333);
@@ -350,8 +351,7 @@ __device__ __forceinline__ double datan2_t(double y, double x, const double2* __
     double a = e.x + (at + e.y);
     a = (ay > ax) ? (1.57079632679489655800e+00 - a) + 6.12323399573676588613e-17 : a;
     a = signbit(x) ? (3.14159265358979311600e+00 - a) + 1.22464679914735317720e-16 : a;
-    a = copysign(a, y);
-    return (isnan(x) || isnan(y)) ? x + y : a;
+    return copysign(a, y);
 }
 
 // z1 / z2 through one reciprocal of |z2|^2 (no Smith scaling: |z2| on this path stays far

@@ -289,6 +289,9 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, int64_t 
 #ifndef DH_FUSED_WAVES
 #define DH_FUSED_WAVES 4    // caps VGPR+AGPR at 128 (4 waves per SIMD)
 #endif
+#ifndef DH_FUSED_WAVES_WIDE
+#define DH_FUSED_WAVES_WIDE 5   // the one-option-per-lane-group variant for large grids (<= 96 VGPRs)
+#endif
 
 // CF entries of one table slot (thread t of TPT): k = t, t + TPT, ..., emitted in increasing k
 // (the k-sums' order) as emit(k, u_k, w_k).
@@ -1162,8 +1165,8 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
 // the same order and with the same lane partition as cos_table_kernel<TPT1> followed by
 // cos_option_kernel<tpt2>, so the two paths give the same bits.
 // ----------------------------------------------------------------------------------------------
-template <int TPT1, int RT>
-__global__ __launch_bounds__(kBlock, DH_FUSED_WAVES) void cos_fused_kernel(PriceArgs A, int tpt2) {
+template <int TPT1, int RT, int WV = DH_FUSED_WAVES>
+__global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(PriceArgs A, int tpt2) {
     // the halt test waits on a global load: taken after the staging barrier, so the load
     // overlaps the prologue instead of delaying it (a halted launch wastes the prologue only)
     const bool halt = halted(A);
@@ -1655,7 +1658,10 @@ int ensure_attrs(dh_ctx* ctx) {
           (const void*)cos_option_kernel<128, kR>, (const void*)cos_option_kernel<256, kR>,
           (const void*)cos_fused_kernel<64, 1>, (const void*)cos_fused_kernel<128, 1>,
           (const void*)cos_fused_kernel<256, 1>, (const void*)cos_fused_kernel<64, kR>,
-          (const void*)cos_fused_kernel<128, kR>, (const void*)cos_fused_kernel<256, kR>})
+          (const void*)cos_fused_kernel<128, kR>, (const void*)cos_fused_kernel<256, kR>,
+          (const void*)cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>,
+          (const void*)cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>,
+          (const void*)cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>})
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
@@ -1708,6 +1714,11 @@ size_t fused_lds_bytes(int N, int cap) {
     return ((size_t)option_lds_doubles(N, cap) + (size_t)cap + kRedDoubles) * sizeof(double);
 }
 
+#ifndef DH_FUSED_WIDE_MIN_BLOCKS
+#define DH_FUSED_WIDE_MIN_BLOCKS 4096
+#endif
+constexpr int64_t kFusedWideMinBlocks = DH_FUSED_WIDE_MIN_BLOCKS;
+
 // One fused launch for the whole request (every group is one tile).
 int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     const int N = A0.N;
@@ -1729,6 +1740,18 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     }
     const dim3 grid((unsigned)blocks), block((unsigned)std::max(t1, t2));
     const bool r1 = tile_r(max_nopt, t2) == 1;
+    // grids of many small blocks (C4: 28,672) gain from a fifth wave per SIMD to overlap the
+    // blocks' latency-bound phases; small grids keep the 4-wave build, whose blocks are shorter
+    // (same arithmetic: only the register allocation differs, so the same bits)
+    if (r1 && blocks >= kFusedWideMinBlocks) {
+        switch (t1) {
+            case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A, t2); break;
+            case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A, t2); break;
+            default: hipLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A, t2); break;
+        }
+        HIP_TRY(hipGetLastError());
+        return DH_OK;
+    }
     switch (t1 * (r1 ? 1 : -1)) {
         case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1>), grid, block, lds, st, A, t2); break;
         case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1>), grid, block, lds, st, A, t2); break;

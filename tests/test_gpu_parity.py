@@ -504,7 +504,8 @@ def _with_path(ctx, path, fn):
     (45, 3, 256, 1, 2048),       # one full 256-option tile, longest series
     (46, 9, 40, 40, 100),        # one option per group, N not a power of two
     (48, 192, 1024, 32, 256),    # 6,144 tables: the split path's table kernel takes one-wave
-                                 # slots (the smaller cases take 128/256-thread slots)
+                                 # slots (the smaller cases take 128/256-thread slots), and the
+                                 # fused path its 5-wave build (grids of >= 4,096 blocks)
 ])
 def test_fused_equals_split_bitwise(dh, seed, P, M, n_T, N):
     """The fused single-launch request kernel and the table + option launches compute every
