@@ -39,7 +39,8 @@ enum {
     DH_E_ARG = -1,               /* invalid argument (null pointer, bad size, N out of range) */
     DH_E_HIP = -2,               /* HIP runtime error (message has the HIP error string) */
     DH_E_NODEV = -3,             /* no usable gfx950 device */
-    DH_E_ALLOC = -4              /* host/device allocation failure */
+    DH_E_ALLOC = -4,             /* host/device allocation failure */
+    DH_E_COMM = -5               /* RCCL failure or librccl not loadable (message has the detail) */
 };
 
 /* strike_mode for surfaces */
@@ -220,6 +221,31 @@ int dh_trunc_range(dh_ctx* ctx, const double* params, const double* K, const dou
 /* chi_k / psi_k for integer k_j on [c,d] within [a,b]: double_heston.py:141-158 */
 int dh_cos_coeffs(dh_ctx* ctx, const int32_t* k, int n, double c, double d, double a, double b,
                   double* chi, double* psi);
+
+/* ---- multi-GPU: RCCL communicator (SURVEY 8(b) dh_allgather_best, 8(e)) --------------------- */
+/* For callers without torch.distributed (the Python layer's dhcos.distributed uses either).  One
+ * communicator per rank, on its context's device and stream; RCCL (librccl.so.1, resolved at run
+ * time) over xGMI.  Rank 0 makes the id and ships its bytes to the other ranks by any means.
+ * Replaces nothing in the reference (single process); it carries the multi-start sharding of
+ * lbfgs_calibrator.py:251-299 across GPUs.                                                      */
+#define DH_COMM_ID_BYTES 128
+typedef struct dh_comm dh_comm;
+int dh_comm_id(unsigned char* id /* [DH_COMM_ID_BYTES] */);
+/* Collective: every rank of `world` calls it with the same id. */
+int dh_comm_create(dh_ctx* ctx, const unsigned char* id, int world, int rank, dh_comm** out);
+int dh_comm_destroy(dh_comm* comm);
+/* buf[n] (host): root's values on every rank (the start x0s and the RNG state after the draws). */
+int dh_comm_broadcast(dh_comm* comm, double* buf, int64_t n, int root);
+/* All-gather of fixed-size per-start records: each rank passes rows x width doubles (its starts;
+ * rows must be equal on every rank, padding rows carry a negative start index), all receives
+ * [world * rows][width] in rank order, and best the winning start index (or -1): the first start,
+ * in start order (column col_start), whose col_fun value is strictly below every earlier one's --
+ * lbfgs_calibrator.py:271-275's rule (NaN never wins), without its re-pricing step.            */
+int dh_allgather_best(dh_comm* comm, const double* rec, int rows, int width, int col_start,
+                      int col_fun, double* all, int* best);
+/* The same selection over records already on the host (no device work). */
+int dh_best_start(const double* all, int64_t rows, int width, int col_start, int col_fun,
+                  int* best);
 
 #ifdef __cplusplus
 }

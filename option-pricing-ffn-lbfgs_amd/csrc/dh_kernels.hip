@@ -33,6 +33,8 @@
 //   Validation ("exact") mode runs cos_exact_kernel instead: per-term CF + sincos in the
 //   reference's operation order, one wave per option.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types only: librccl is resolved at run time (dlopen)
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <chrono>
@@ -3199,4 +3201,183 @@ extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
             g[(size_t)st * kN + i] = (fl[i + 1] - fl[0]) / dx[(size_t)st * kN + i];
     }
     return DH_OK;
+}
+
+// ----------------------------------------------------------------------------------------------
+// multi-GPU: an RCCL communicator for callers without torch.distributed (SURVEY 8(b)'s
+// dh_allgather_best, 8(e) multi-start sharding).  librccl.so.1 is resolved at run time: with
+// torch imported that is torch's own copy (the same soname), otherwise ROCm's, so a process holds
+// one RCCL either way and the library does not link it.
+// ----------------------------------------------------------------------------------------------
+namespace {
+
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+const RcclApi& rccl() {
+    static const RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            a.err = std::string("librccl not found: ") + (e ? e : "");
+            return a;
+        }
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            if (!fn && a.err.empty()) a.err = std::string("librccl lacks ") + name;
+        };
+        sym(a.get_unique_id, "ncclGetUniqueId");
+        sym(a.comm_init_rank, "ncclCommInitRank");
+        sym(a.all_gather, "ncclAllGather");
+        sym(a.broadcast, "ncclBroadcast");
+        sym(a.comm_destroy, "ncclCommDestroy");
+        sym(a.error_string, "ncclGetErrorString");
+        a.ok = a.err.empty();
+        return a;
+    }();
+    return api;
+}
+
+int nccl_fail(const char* what, ncclResult_t r) {
+    return fail(DH_E_COMM, std::string(what) + ": " + rccl().error_string(r));
+}
+
+#define NCCL_TRY(expr)                                       \
+    do {                                                     \
+        const ncclResult_t _r = (expr);                      \
+        if (_r != ncclSuccess) return nccl_fail(#expr, _r);  \
+    } while (0)
+
+}  // namespace
+
+struct dh_comm {
+    dh_ctx* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    int world = 0, rank = 0;
+    DevBuf send, recv;
+};
+
+extern "C" int dh_comm_id(unsigned char* id) {
+    if (!id) return fail(DH_E_ARG, "id is null");
+    const RcclApi& R = rccl();
+    if (!R.ok) return fail(DH_E_COMM, R.err);
+    ncclUniqueId u;
+    NCCL_TRY(R.get_unique_id(&u));
+    static_assert(sizeof(u) == DH_COMM_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(id, &u, sizeof(u));
+    return DH_OK;
+}
+
+extern "C" int dh_comm_create(dh_ctx* ctx, const unsigned char* id, int world, int rank,
+                              dh_comm** out) {
+    if (!ctx || !id || !out) return fail(DH_E_ARG, "null argument");
+    *out = nullptr;
+    if (world < 1 || rank < 0 || rank >= world) return fail(DH_E_ARG, "rank / world out of range");
+    const RcclApi& R = rccl();
+    if (!R.ok) return fail(DH_E_COMM, R.err);
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    dh_comm* c = new (std::nothrow) dh_comm();
+    if (!c) return fail(DH_E_ALLOC, "comm alloc");
+    const ncclResult_t r = R.comm_init_rank(&c->comm, world, u, rank);   // joins every rank
+    if (r != ncclSuccess) {
+        delete c;
+        return nccl_fail("ncclCommInitRank", r);
+    }
+    c->ctx = ctx;
+    c->world = world;
+    c->rank = rank;
+    *out = c;
+    return DH_OK;
+}
+
+extern "C" int dh_comm_destroy(dh_comm* c) {
+    if (!c) return DH_OK;
+    int rc = DH_OK;
+    {
+        DeviceScope dev_scope(c->ctx->device);
+        if (c->comm) {
+            const ncclResult_t r = rccl().comm_destroy(c->comm);
+            if (r != ncclSuccess) rc = nccl_fail("ncclCommDestroy", r);
+        }
+        c->send.release();
+        c->recv.release();
+    }
+    delete c;
+    return rc;
+}
+
+extern "C" int dh_comm_broadcast(dh_comm* c, double* buf, int64_t n, int root) {
+    if (!c || (n > 0 && !buf)) return fail(DH_E_ARG, "null argument");
+    if (root < 0 || root >= c->world) return fail(DH_E_ARG, "root out of range");
+    if (n <= 0) return DH_OK;
+    DeviceScope dev_scope(c->ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
+    const size_t bytes = (size_t)n * sizeof(double);
+    hipStream_t st = c->ctx->stream;
+    HIP_TRY(c->send.reserve(bytes));
+    if (c->rank == root) HIP_TRY(hipMemcpyAsync(c->send.ptr, buf, bytes, hipMemcpyHostToDevice, st));
+    NCCL_TRY(rccl().broadcast(c->send.ptr, c->send.ptr, (size_t)n, ncclFloat64, root, c->comm, st));
+    HIP_TRY(hipMemcpyAsync(buf, c->send.ptr, bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return DH_OK;
+}
+
+extern "C" int dh_best_start(const double* all, int64_t rows, int width, int col_start,
+                             int col_fun, int* best) {
+    if (!best || (rows > 0 && !all)) return fail(DH_E_ARG, "null argument");
+    if (width < 1 || col_start < 0 || col_start >= width || col_fun < 0 || col_fun >= width)
+        return fail(DH_E_ARG, "column out of range");
+    // lbfgs_calibrator.py:271-275: starts in order, best_loss = inf, strict < (NaN never wins);
+    // rows with a negative start index are padding
+    std::vector<std::pair<double, double>> by_start;           // (start, fun)
+    by_start.reserve((size_t)std::max<int64_t>(rows, 0));
+    for (int64_t i = 0; i < rows; ++i) {
+        const double s = all[i * width + col_start];
+        if (s >= 0.0) by_start.emplace_back(s, all[i * width + col_fun]);
+    }
+    std::stable_sort(by_start.begin(), by_start.end(),
+                     [](const auto& a, const auto& b) { return a.first < b.first; });
+    double best_loss = __builtin_huge_val();
+    *best = -1;
+    for (const auto& e : by_start)
+        if (e.second < best_loss) {
+            best_loss = e.second;
+            *best = (int)e.first;
+        }
+    return DH_OK;
+}
+
+extern "C" int dh_allgather_best(dh_comm* c, const double* rec, int rows, int width,
+                                 int col_start, int col_fun, double* all, int* best) {
+    if (!c || !all || !best || (rows > 0 && !rec)) return fail(DH_E_ARG, "null argument");
+    if (rows < 0 || width < 1) return fail(DH_E_ARG, "rows / width out of range");
+    const size_t per = (size_t)rows * width;
+    if (per > 0) {
+        DeviceScope dev_scope(c->ctx->device);
+        if (dev_scope.rc) return dev_scope.rc;
+        hipStream_t st = c->ctx->stream;
+        HIP_TRY(c->send.reserve(per * sizeof(double)));
+        HIP_TRY(c->recv.reserve(per * c->world * sizeof(double)));
+        HIP_TRY(hipMemcpyAsync(c->send.ptr, rec, per * sizeof(double), hipMemcpyHostToDevice, st));
+        NCCL_TRY(rccl().all_gather(c->send.ptr, c->recv.ptr, per, ncclFloat64, c->comm, st));
+        HIP_TRY(hipMemcpyAsync(all, c->recv.ptr, per * c->world * sizeof(double),
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return dh_best_start(all, (int64_t)rows * c->world, width, col_start, col_fun, best);
 }

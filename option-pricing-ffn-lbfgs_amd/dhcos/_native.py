@@ -91,6 +91,12 @@ SIGNATURES = {
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
     "dh_cos_coeffs": (C.c_int, [_vp, _i32p, C.c_int, C.c_double, C.c_double, C.c_double,
                                 C.c_double, _dp, _dp]),
+    "dh_comm_id": (C.c_int, [_vp]),
+    "dh_comm_create": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "dh_comm_destroy": (C.c_int, [_vp]),
+    "dh_comm_broadcast": (C.c_int, [_vp, _vp, C.c_int64, C.c_int]),
+    "dh_allgather_best": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _i32p]),
+    "dh_best_start": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.c_int, _i32p]),
 }
 
 
@@ -411,6 +417,73 @@ class Surface:
                                           _vp(stream) if stream else None))
 
 
+COMM_ID_BYTES = 128
+
+
+def comm_id() -> bytes:
+    """dh_comm_id: a fresh RCCL unique id (rank 0), to be shipped to every rank."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(load().dh_comm_id(C.cast(buf, _vp)))
+    return buf.raw
+
+
+def best_start(records, col_start, col_fun) -> int:
+    """dh_best_start: the reference's strict-< best start (lbfgs_calibrator.py:271-275) over
+    per-start rows (negative start index = padding); -1 if none."""
+    rec = np.ascontiguousarray(records, dtype=np.float64)
+    rows, width = (rec.shape[0], rec.shape[1]) if rec.ndim == 2 else (0, 1)
+    best = C.c_int32(-2)
+    _check(load().dh_best_start(rec.ctypes.data if rows else None, rows, width, int(col_start),
+                                int(col_fun), C.byref(best)))
+    return best.value
+
+
+class Comm:
+    """dh_comm: an RCCL communicator over the ranks' contexts (one per rank, its device and
+    stream), for multi-start sharding without torch.distributed.  Collective construction: every
+    rank passes rank 0's ``comm_id()`` bytes."""
+
+    def __init__(self, ctx: "Context", uid: bytes, world: int, rank: int):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"comm id must be {COMM_ID_BYTES} bytes")
+        self.ctx, self.world, self.rank = ctx, int(world), int(rank)
+        self._uid = C.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        h = _vp()
+        _check(load().dh_comm_create(ctx.handle, C.cast(self._uid, _vp), self.world, self.rank,
+                                     C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            h, self._h = self._h, None
+            _check(load().dh_comm_destroy(h))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def broadcast(self, buf, root: int = 0) -> np.ndarray:
+        """root's float64 values on every rank (in place on a contiguous array; returned)."""
+        out = np.ascontiguousarray(buf, dtype=np.float64)
+        _check(load().dh_comm_broadcast(self._h, out.ctypes.data if out.size else None, out.size,
+                                        int(root)))
+        return out
+
+    def allgather_best(self, records, col_start: int, col_fun: int):
+        """records [rows, width] of this rank (same rows on every rank) -> ([world * rows, width]
+        in rank order, the strict-< best start or -1)."""
+        rec = np.ascontiguousarray(records, dtype=np.float64)
+        rows, width = rec.shape
+        out = np.empty((self.world * rows, width))
+        best = C.c_int32(-2)
+        _check(load().dh_allgather_best(self._h, rec.ctypes.data if rec.size else None, rows,
+                                        width, int(col_start), int(col_fun),
+                                        out.ctypes.data, C.byref(best)))
+        return out, best.value
+
+
 def gen_draw(n_samples, lo, hi, n_opt, alpha, spot0, ret_mu, ret_sigma, noise_sigma):
     """dh_gen_draw on NumPy's global legacy RandomState: draws the generator's samples natively
     and advances np.random's state exactly as the reference's per-sample calls would.
@@ -470,4 +543,5 @@ def default_context(device: int | None = None) -> Context:
 
 __all__ = ["gen_draw", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "STRIKE_ABSOLUTE",
-           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "LIB_PATH", "SIGNATURES"]
+           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "LIB_PATH", "SIGNATURES",
+           "Comm", "comm_id", "best_start", "COMM_ID_BYTES"]

@@ -18,7 +18,9 @@ is exchanged: the shards are independent and each rank drives its own GPU.
     reference output.  Every rank's ``np.random`` ends where rank 0's draws left it.
 
 Only collectives on small host-side records and (generator) the price block are used; the COS
-kernels never wait on another rank.
+kernels never wait on another rank.  The collectives run over ``torch.distributed`` (a process
+group) or, for callers without torch, over the library's own RCCL communicator
+(``comm=_native.Comm``: dh_comm_broadcast / dh_allgather_best).
 """
 from __future__ import annotations
 
@@ -46,14 +48,20 @@ def _comm_device(group=None, device=None):
     return torch.device("cpu")
 
 
-def _world(group=None):
+def _world(group=None, comm=None):
+    if comm is not None:
+        return comm.rank, comm.world
     if not (dist.is_available() and dist.is_initialized()):
         return 0, 1
     return dist.get_rank(group), dist.get_world_size(group)
 
 
-def _broadcast_f64(arr, shape, group=None, device=None):
+def _broadcast_f64(arr, shape, group=None, device=None, comm=None):
     """Broadcast a float64 array from rank 0 (bit-exact)."""
+    if comm is not None:
+        buf = (np.array(arr, dtype=np.float64).reshape(shape) if comm.rank == 0
+               else np.zeros(shape))
+        return comm.broadcast(buf, 0)
     dev = _comm_device(group, device)
     t = torch.empty(shape, dtype=torch.float64, device=dev)
     if dist.get_rank(group) == 0:
@@ -73,6 +81,7 @@ def _encode(s, out, t0, stats=(0, np.inf)):
     rec = np.zeros(_REC_I64, dtype=np.int64)
     d = np.zeros(_REC, dtype=np.float64)
     d[1] = s
+    d[2] = np.nan                      # no outcome: never the best (dh_allgather_best's rule)
     d[7], d[8] = stats
     if out is not None:
         res, t_done = out
@@ -99,22 +108,27 @@ def _decode(rec):
                            t_rel=float(d[6]), x=d[9:].copy(), message=msg), stats
 
 
-def gather_start_records(local, n_starts, group=None, device=None):
+def gather_start_records(local, n_starts, group=None, device=None, comm=None):
     """All-gather the per-start records of every rank -> ([n_starts] decoded outcomes,
     [n_starts] (n_calls, best_loss))."""
-    rank, world = _world(group)
+    rank, world = _world(group, comm)
     n_max = (n_starts + world - 1) // world
     buf = np.zeros((n_max, _REC_I64), dtype=np.int64)
     buf[:, :_REC] = np.full(_REC, -1.0).view(np.int64)      # padding rows: start index -1
     for i, rec in enumerate(local):
         buf[i] = rec
-    dev = _comm_device(group, device)
-    mine = torch.from_numpy(buf).to(dev)
-    parts = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(parts, mine, group=group)
+    if comm is not None:              # RCCL moves the records' bytes unchanged (a copy)
+        allr, _ = comm.allgather_best(buf.view(np.float64), col_start=1, col_fun=2)
+        parts = list(allr.view(np.int64).reshape(world, n_max, _REC_I64))
+    else:
+        dev = _comm_device(group, device)
+        mine = torch.from_numpy(buf).to(dev)
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine, group=group)
+        parts = [p.cpu().numpy() for p in parts]
     table, stats = [None] * n_starts, [(0, np.inf)] * n_starts
     for p in parts:
-        for row in p.cpu().numpy():
+        for row in p:
             s, out, st = _decode(row)
             if 0 <= s < n_starts:
                 table[s], stats[s] = out, st
@@ -136,12 +150,13 @@ def _set_rng_state_vec(v):
 
 def calibrate_sharded(cal: DoubleHestonJumpCalibrator, maxiter: int = 300, multi_start: int = 3,
                       *, group=None, x0s=None, x0=None,
-                      driver: str = "scipy") -> CalibrationResult:
+                      driver: str = "scipy", comm=None) -> CalibrationResult:
     """``cal.calibrate(maxiter, multi_start, x0s=x0s, x0=x0, driver=driver)`` with the starts
-    sharded over the process group.  Every rank returns the same ``CalibrationResult`` and ends
-    with the same ``cal.n_calls`` / ``cal.best_loss`` and ``np.random`` state."""
-    rank, world = _world(group)
-    if world == 1:
+    sharded over the process group (or the ranks of ``comm``, a ``_native.Comm``).  Every rank
+    returns the same ``CalibrationResult`` and ends with the same ``cal.n_calls`` /
+    ``cal.best_loss`` and ``np.random`` state."""
+    rank, world = _world(group, comm)
+    if world == 1 and comm is None:
         return cal.calibrate(maxiter=maxiter, multi_start=multi_start, x0s=x0s, x0=x0,
                              driver=driver)
     if driver not in ("scipy", "device"):
@@ -154,7 +169,7 @@ def calibrate_sharded(cal: DoubleHestonJumpCalibrator, maxiter: int = 300, multi
             x0s = cal.start_points(multi_start, x0)
         block = np.concatenate([np.asarray(x0s, dtype=np.float64).reshape(-1),
                                 _rng_state_vec()])
-    block = _broadcast_f64(block, (multi_start * N_PARAMS + 627,), group, dev)
+    block = _broadcast_f64(block, (multi_start * N_PARAMS + 627,), group, dev, comm)
     x0s = block[:multi_start * N_PARAMS].reshape(multi_start, N_PARAMS)
     _set_rng_state_vec(block[multi_start * N_PARAMS:])
     mine = start_shard(multi_start, rank, world)
@@ -163,7 +178,7 @@ def calibrate_sharded(cal: DoubleHestonJumpCalibrator, maxiter: int = 300, multi
     stats_local = getattr(cal, "start_stats", None) if mine else []
     local = [_encode(s, o, t0, stats_local[i] if stats_local else (0, np.inf))
              for i, (s, o) in enumerate(zip(mine, outcomes))]
-    table, stats = gather_start_records(local, multi_start, group, dev)
+    table, stats = gather_start_records(local, multi_start, group, dev, comm)
     if multi_start > 0:     # the per-start resets (:253-254): the state after the last start
         cal.n_calls, cal.best_loss = stats[multi_start - 1]
 

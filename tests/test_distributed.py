@@ -159,3 +159,42 @@ def test_resolve_device(monkeypatch):
     assert _native.resolve_device() == 0            # no process group: device 0
     monkeypatch.setenv("DHCOS_DEVICE", "2")
     assert _native.resolve_device() == 2
+
+
+def _reference_best(rows):
+    """lbfgs_calibrator.py:271-275: starts in order, best_loss = inf, strict <."""
+    best, best_loss = -1, np.inf
+    for s, fun in sorted(((r[1], r[2]) for r in rows if r[1] >= 0), key=lambda t: t[0]):
+        if fun < best_loss:
+            best, best_loss = int(s), fun
+    return best
+
+
+def test_best_start_matches_reference_rule():
+    """dh_best_start (host only, the selection dh_allgather_best applies after its RCCL gather):
+    start order, strict <, NaN and inf never win, padding rows (start < 0) ignored, ties go to the
+    earlier start -- on records gathered in rank order, not start order."""
+    from dhcos import _native
+    rs = np.random.RandomState(7)
+    for trial in range(200):
+        n = rs.randint(0, 20)
+        rows = np.zeros((n + 3, 5))
+        rows[:, 1] = -1.0                                   # padding
+        starts = rs.permutation(n)
+        for i, s in enumerate(starts):
+            rows[i, 1] = s
+            rows[i, 2] = rs.choice([np.nan, np.inf, 1e10, 0.5, 0.25, rs.rand()])
+        rs.shuffle(rows)
+        assert _native.best_start(rows, 1, 2) == _reference_best(rows), (trial, rows)
+    assert _native.best_start(np.zeros((0, 5)), 1, 2) == -1
+    with pytest.raises(_native.NativeError):
+        _native.best_start(np.zeros((2, 3)), 1, 5)
+
+
+def test_missing_outcome_record_never_wins():
+    """A start without an outcome travels with fun = NaN, so the native selection skips it."""
+    rec = D._encode(3, None, 0.0)
+    d = rec[:D._REC].view(np.float64)
+    assert d[1] == 3 and np.isnan(d[2])
+    s, out, stats = D._decode(rec)
+    assert s == 3 and out is None and stats == (0, np.inf)
