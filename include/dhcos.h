@@ -129,6 +129,16 @@ int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params
  * reference's NumPy uses, so f equals compute_loss(x0) bit for bit; NULL = libm exp / tanh here. */
 int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0, const double* model, int S,
                   double S0, double r, int N, double L, double* f, double* g, double* low);
+/* The same request in two halves, so a host driver can run one group of starts' optimizer steps
+ * while another group's request is on the device: begin forms the records into slot (0 or 1; each
+ * slot owns its pinned buffers) and enqueues the request on the context's stream, then returns;
+ * end waits for that slot's request and writes f, g, low as dh_surface_fg would (the same bits:
+ * a start's values depend only on its own x0).  A slot holds one request at a time; requests
+ * run in enqueue order; 14 S <= 1024 (larger: dh_surface_fg).                                   */
+int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const double* x0, const double* model,
+                        int S, double S0, double r, int N, double L, int slot);
+int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, double* f, double* g,
+                      double* low);
 
 /* ---- device-resident multi-start L-BFGS-B ------------------------------------------------- */
 /* Runs S independent L-BFGS-B starts (no bounds) on the surface's calibration loss without a

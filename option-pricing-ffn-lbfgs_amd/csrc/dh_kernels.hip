@@ -1578,6 +1578,15 @@ struct dh_ctx {
     HostBuf h_pairs;           // zero-copy inputs / outputs of small dh_price_pairs calls
     DevBuf lb_state, lb_rec, lb_sse, lb_bad, lb_live, lb_done, lb_x0;   // dh_calibrate_lbfgs
     HostBuf h_lb;              // finished flags / live list of dh_calibrate_lbfgs
+    // the two in-flight slots of dh_surface_fg_begin / _end: zero-copy records in, sse / n_bad
+    // out, the host-side Feller terms and FD steps, and the request's completion event
+    struct FgSlot {
+        HostBuf h_params, h_loss;
+        std::vector<double> pen, dx;
+        int S = 0, M = 0;
+        bool pending = false;
+        hipEvent_t done = nullptr;
+    } fg[2];
     DevBuf lb_trace, lb_trace_n;   // diagnostic request trace of dh_calibrate_lbfgs
     hipEvent_t lb_ev[2] = {nullptr, nullptr};   // chunk-completion events of dh_calibrate_lbfgs
     int64_t lb_trace_cap = 0;
@@ -1938,6 +1947,11 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     ctx->h_pairs.release();
     for (hipEvent_t e : ctx->lb_ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& F : ctx->fg) {
+        F.h_params.release();
+        F.h_loss.release();
+        if (F.done) (void)hipEventDestroy(F.done);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return DH_OK;
@@ -3137,24 +3151,17 @@ extern "C" int dh_loss_batch(dh_ctx* ctx, const double* x, int S, const double* 
 // ----------------------------------------------------------------------------------------------
 // function + FD-gradient requests for the host (SciPy) driver
 // ----------------------------------------------------------------------------------------------
-extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
-                             const double* model, int S, double S0, double r, int N, double L,
-                             double* f, double* g, double* low) {
-    if (!ctx || !s || (S > 0 && (!x0 || !f || !g || !low))) return fail(DH_E_ARG, "null argument");
-    if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
-    if (s->M == 0) return fail(DH_E_ARG, "empty market (the loss is NaN)");
-    if (S < 0) return fail(DH_E_ARG, "S < 0");
-    if (S == 0) return DH_OK;
+namespace {
+
+// The request's points (scipy/optimize/_numdiff.py:498-511: x0, then x0 + h_i e_i with h = 1e-8,
+// or sqrt(eps) sign(x) max(1, |x|) where the absolute step vanishes), their model params (exp /
+// tanh / identity, lbfgs_calibrator.py:62-87) and Feller penalties (:113-116): rec [S * 14][16],
+// pen [S * 14], dx [S][13].  The caller passes the model params of x0 and x0 + h (model:
+// [2][S][13]) when they must be the bits of its own exp / tanh (NumPy's, as the reference's
+// transform_params); otherwise they come from libm here.
+void fg_points(const double* x0, const double* model, int S, double S0, double r, double* rec,
+               double* pen, double* dx) {
     constexpr int kP = dhlb::kPts, kN = dhlb::kN;
-    const size_t P = (size_t)S * kP;
-    std::vector<double> rec(P * DH_PARAM_STRIDE), pen(P), dx((size_t)S * kN), sse(P);
-    std::vector<int32_t> bad(P);
-    // the request's points (scipy/optimize/_numdiff.py:498-511: x0, then x0 + h_i e_i with
-    // h = 1e-8, or sqrt(eps) sign(x) max(1, |x|) where the absolute step vanishes), their model
-    // params (exp / tanh / identity, lbfgs_calibrator.py:62-87) and Feller penalties (:113-116).
-    // The caller passes the model params of x0 and x0 + h (model: [2][S][13]) when they must be
-    // the bits of its own exp / tanh (NumPy's, as the reference's transform_params); otherwise
-    // they come from libm here.
     for (int st = 0; st < S; ++st) {
         const double* x = x0 + (size_t)st * kN;
         double pb[kN], pp[kN];
@@ -3174,7 +3181,7 @@ extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
             }
         }
         for (int t = 0; t < kP; ++t) {
-            double* o = rec.data() + ((size_t)st * kP + t) * DH_PARAM_STRIDE;
+            double* o = rec + ((size_t)st * kP + t) * DH_PARAM_STRIDE;
             for (int i = 0; i < kN; ++i) o[i] = (i == t - 1) ? pp[i] : pb[i];
             const double v1 = o[3] * o[3] - 2.0 * o[1] * o[2];
             const double v2 = o[8] * o[8] - 2.0 * o[6] * o[7];
@@ -3184,15 +3191,18 @@ extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
             o[15] = 0.0;
         }
     }
-    int rc = dh_surface_loss(ctx, s, rec.data(), (int)P, N, L, sse.data(), bad.data(), nullptr);
-    if (rc) return rc;
-    // loss = n_bad ? 1e10 : sse / M + Feller (lbfgs_calibrator.py:152-166); f, the FD gradient
-    // (f_i - f_0) / dx_i as SciPy forms it, and the smallest valid loss of the request
+}
+
+// loss = n_bad ? 1e10 : sse / M + Feller (lbfgs_calibrator.py:152-166); f, the FD gradient
+// (f_i - f_0) / dx_i as SciPy forms it, and the smallest valid loss of the request
+void fg_finish(int S, int M, const double* sse, const int32_t* bad, const double* pen,
+               const double* dx, double* f, double* g, double* low) {
+    constexpr int kP = dhlb::kPts, kN = dhlb::kN;
     for (int st = 0; st < S; ++st) {
         double lo = __builtin_huge_val(), fl[kP];
         for (int t = 0; t < kP; ++t) {
             const size_t i = (size_t)st * kP + t;
-            fl[t] = bad[i] > 0 ? kInvalidLoss : sse[i] / (double)s->M + pen[i];
+            fl[t] = bad[i] > 0 ? kInvalidLoss : sse[i] / (double)M + pen[i];
             if (fl[t] == fl[t] && fl[t] != kInvalidLoss && fl[t] < lo) lo = fl[t];
         }
         f[st] = fl[0];
@@ -3200,6 +3210,100 @@ extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
         for (int i = 0; i < kN; ++i)
             g[(size_t)st * kN + i] = (fl[i + 1] - fl[0]) / dx[(size_t)st * kN + i];
     }
+}
+
+int fg_check(dh_ctx* ctx, const dh_surface* s, int S) {
+    if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
+    if (s->M == 0) return fail(DH_E_ARG, "empty market (the loss is NaN)");
+    if (S < 0) return fail(DH_E_ARG, "S < 0");
+    (void)ctx;
+    return DH_OK;
+}
+
+}  // namespace
+
+extern "C" int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0,
+                             const double* model, int S, double S0, double r, int N, double L,
+                             double* f, double* g, double* low) {
+    if (!ctx || !s || (S > 0 && (!x0 || !f || !g || !low))) return fail(DH_E_ARG, "null argument");
+    int rc = fg_check(ctx, s, S);
+    if (rc) return rc;
+    if (S == 0) return DH_OK;
+    const size_t P = (size_t)S * dhlb::kPts;
+    std::vector<double> rec(P * DH_PARAM_STRIDE), pen(P), dx((size_t)S * dhlb::kN), sse(P);
+    std::vector<int32_t> bad(P);
+    fg_points(x0, model, S, S0, r, rec.data(), pen.data(), dx.data());
+    rc = dh_surface_loss(ctx, s, rec.data(), (int)P, N, L, sse.data(), bad.data(), nullptr);
+    if (rc) return rc;
+    fg_finish(S, s->M, sse.data(), bad.data(), pen.data(), dx.data(), f, g, low);
+    return DH_OK;
+}
+
+extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const double* x0,
+                                   const double* model, int S, double S0, double r, int N,
+                                   double L, int slot) {
+    if (!ctx || !s || (S > 0 && !x0)) return fail(DH_E_ARG, "null argument");
+    if (slot < 0 || slot > 1) return fail(DH_E_ARG, "slot must be 0 or 1");
+    int rc = fg_check(ctx, s, S);
+    if (rc) return rc;
+    rc = check_N(N);
+    if (rc) return rc;
+    auto& F = ctx->fg[slot];
+    if (F.pending) return fail(DH_E_ARG, "slot has a request in flight (call dh_surface_fg_end)");
+    const size_t P = (size_t)S * dhlb::kPts;
+    if (P > (size_t)kZeroCopyMaxSets)
+        return fail(DH_E_ARG, "too many starts for one asynchronous request (use dh_surface_fg)");
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
+    // the loss launch grows the context's device scratch when this request is larger than any
+    // before; a grow frees the old buffers, so let the other slot's request finish first
+    auto& O = ctx->fg[1 - slot];
+    if (O.pending && (P * s->n_tiles * 8 > ctx->part_sse.cap ||
+                      P * kCounterStride * 4 > ctx->counter.cap))
+        HIP_TRY(hipEventSynchronize(O.done));
+    HIP_TRY(F.h_params.reserve(P * DH_PARAM_STRIDE * 8));
+    HIP_TRY(F.h_loss.reserve(P * 12));
+    F.pen.resize(P);
+    F.dx.resize((size_t)S * dhlb::kN);
+    if (!F.done) HIP_TRY(hipEventCreateWithFlags(&F.done, hipEventDisableTiming));
+    F.S = S;
+    F.M = s->M;
+    if (S == 0) {
+        HIP_TRY(hipEventRecord(F.done, ctx->stream));
+        F.pending = true;
+        return DH_OK;
+    }
+    fg_points(x0, model, S, S0, r, (double*)F.h_params.ptr, F.pen.data(), F.dx.data());
+    rc = dh_surface_loss_dev(ctx, s, (const double*)F.h_params.dptr, (int)P, N, L,
+                             (double*)F.h_loss.dptr, (int32_t*)((double*)F.h_loss.dptr + P),
+                             nullptr, ctx->stream);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(F.done, ctx->stream));
+    F.pending = true;
+    return DH_OK;
+}
+
+extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, double* f, double* g,
+                                 double* low) {
+    if (!ctx || !s) return fail(DH_E_ARG, "null argument");
+    if (slot < 0 || slot > 1) return fail(DH_E_ARG, "slot must be 0 or 1");
+    auto& F = ctx->fg[slot];
+    if (!F.pending) return fail(DH_E_ARG, "no request in flight in this slot");
+    if (F.S > 0 && (!f || !g || !low)) return fail(DH_E_ARG, "null argument");
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
+    for (;;) {                          // busy-wait: an optimizer iteration waits on it
+        const hipError_t e = hipEventQuery(F.done);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) {
+            F.pending = false;
+            return fail(DH_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
+        }
+    }
+    F.pending = false;
+    const size_t P = (size_t)F.S * dhlb::kPts;
+    fg_finish(F.S, F.M, (const double*)F.h_loss.ptr, (const int32_t*)((double*)F.h_loss.ptr + P),
+              F.pen.data(), F.dx.data(), f, g, low);
     return DH_OK;
 }
 

@@ -86,6 +86,9 @@ SIGNATURES = {
                                 C.c_double, C.c_int, C.c_double, _dp, _i32p]),
     "dh_surface_fg": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, C.c_double, C.c_double, C.c_int,
                                 C.c_double, _vp, _vp, _vp]),
+    "dh_surface_fg_begin": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, C.c_double, C.c_double,
+                                      C.c_int, C.c_double, C.c_int]),
+    "dh_surface_fg_end": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, _vp]),
     "dh_price_pairs": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
@@ -329,6 +332,7 @@ class Surface:
                                         C.byref(h)))
         self._h = h
         self.M = M
+        self._fg_s = [0, 0]              # starts of the request in each fg_begin slot
         m, nt = C.c_int32(0), C.c_int32(0)
         _check(load().dh_surface_size(h, C.byref(m), C.byref(nt)))
         self.n_tiles = nt.value
@@ -402,6 +406,30 @@ class Surface:
                                         None if model is None else model.ctypes.data, S,
                                         float(S0), float(r), int(N), float(L), f.ctypes.data,
                                         g.ctypes.data, low.ctypes.data))
+        return f, g, low
+
+    def fg_begin(self, X0, S0, r, N=128, L=10.0, model=None, slot=0):
+        """dh_surface_fg_begin: enqueue fg(X0) into slot 0 or 1 and return at once; the slot
+        keeps the request until fg_end(slot)."""
+        X0 = _f64(X0).reshape(-1, 13)
+        S = X0.shape[0]
+        if model is not None:
+            model = _f64(model)
+            if model.shape != (2, S, 13):
+                raise ValueError(f"model must be [2, {S}, 13], got {model.shape}")
+        with self.ctx._lock:
+            _check(load().dh_surface_fg_begin(self.ctx.handle, self._h, X0.ctypes.data,
+                                              None if model is None else model.ctypes.data, S,
+                                              float(S0), float(r), int(N), float(L), int(slot)))
+        self._fg_s[slot] = S
+
+    def fg_end(self, slot=0):
+        """dh_surface_fg_end: wait for slot's request -> (f [S], g [S, 13], low [S])."""
+        S = self._fg_s[slot]
+        f, g, low = np.empty(S), np.empty((S, 13)), np.empty(S)
+        with self.ctx._lock:
+            _check(load().dh_surface_fg_end(self.ctx.handle, self._h, int(slot), f.ctypes.data,
+                                            g.ctypes.data, low.ctypes.data))
         return f, g, low
 
     # device-pointer variants (torch tensors or raw device addresses)

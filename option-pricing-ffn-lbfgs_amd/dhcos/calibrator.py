@@ -462,12 +462,35 @@ class _StartState:
         self.best_loss = np.inf
 
 
-def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: bool = True):
+def _pipeline_surface(cal, n_starts):
+    """The surface the two-group pipelined loop may use, or None: subclassed losses, markets
+    without a surface, one start, or groups too large for one asynchronous request keep the
+    lockstep loop."""
+    if n_starts < 2 or -(-n_starts // 2) * (N_PARAMS + 1) > _native_async_max_sets():
+        return None
+    cls = type(cal)
+    if (not isinstance(cal, DoubleHestonJumpCalibrator)
+            or cls.fg_batch is not DoubleHestonJumpCalibrator.fg_batch
+            or cls.loss_batch is not DoubleHestonJumpCalibrator.loss_batch
+            or not len(cal.market_options)):
+        return None
+    return cal._get_surface()
+
+
+def _native_async_max_sets():
+    return 1024                        # dh_surface_fg_begin: 14 S <= 1024 (include/dhcos.h)
+
+
+def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: bool = True,
+               pipeline: bool = True):
     """Run one L-BFGS-B per x0; returns [(OptimizeResult, t_done) | None] in start order.
 
     lockstep: every live start's function+gradient request shares one launch (S = 14 x live
-    starts); otherwise the starts run one after the other.  A start's values depend only on its
-    own x (the kernels are batch-composition invariant), so both give the same results."""
+    starts); otherwise the starts run one after the other.  pipeline (with lockstep, >= 2
+    starts): the starts form two groups whose requests alternate on the device, so one group's
+    setulb steps run on the host while the other's request runs (_advance_pipelined).  A start's
+    values depend only on its own x (the kernels are batch-composition invariant), so all three
+    give the same results."""
     n = len(x0s)
     outcomes = [None] * n
     if n == 0:
@@ -475,8 +498,12 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
     gens = [lbfgsb_steps(x0, maxiter, _MAXFUN) for x0 in x0s]
     states = [_StartState() for _ in range(n)]
     order = [list(range(n))] if lockstep else [[s] for s in range(n)]
+    surf = _pipeline_surface(cal, n) if (lockstep and pipeline) else None
     with _single_threaded_blas():
-        _advance(cal, gens, states, order, outcomes)
+        if surf is not None:
+            _advance_pipelined(cal, surf, gens, states, outcomes)
+        else:
+            _advance(cal, gens, states, order, outcomes)
     cal.start_stats = [(st.n_calls, st.best_loss) for st in states]
     last = states[-1]
     cal.n_calls, cal.best_loss = last.n_calls, last.best_loss   # state after the last start
@@ -517,6 +544,65 @@ def _advance(cal, gens, states, order, outcomes):
                     del pending[sid]
                 except Exception:      # noqa: BLE001 -- reference: except -> continue
                     del pending[sid]
+    cal.lockstep_launches = launches
+
+
+def _consume(states, gens, pending, outcomes, ids, f0, G, lows):
+    """A request's results to its starts' generators (the bookkeeping of _advance)."""
+    for j, sid in enumerate(ids):
+        st = states[sid]
+        st.n_calls += N_PARAMS + 1
+        if lows[j] < st.best_loss:
+            st.best_loss = lows[j]
+        try:
+            pending[sid] = gens[sid].send((f0[j], G[j]))
+        except StopIteration as stop:
+            outcomes[sid] = (stop.value, time.time())
+            del pending[sid]
+        except Exception:      # noqa: BLE001 -- reference: except -> continue
+            del pending[sid]
+
+
+def _advance_pipelined(cal, surf, gens, states, outcomes):
+    """run_starts' two-group loop: starts of even and odd index form groups 0 and 1, each with
+    its own request slot (dh_surface_fg_begin / _end).  Group k's results are consumed, its next
+    request enqueued behind the other group's, then the other group's results are awaited: the
+    host's setulb steps of one group overlap the device's request of the other.  The per-start
+    values and bookkeeping are _advance's."""
+    n = len(gens)
+    groups = [[s for s in range(n) if s % 2 == k] for k in (0, 1)]
+    pending = {sid: next(gens[sid]) for sid in range(n)}
+    inflight = [None, None]
+    launches = 0
+
+    def submit(k):
+        ids = [sid for sid in groups[k] if sid in pending]
+        inflight[k] = None
+        if not ids:
+            return
+        X0 = np.stack([pending[sid] for sid in ids])
+        try:
+            model = fd_models(X0)
+        except Exception:          # reference: except -> continue (the starts are dropped)
+            for sid in ids:
+                gens[sid].close()
+                del pending[sid]
+            return
+        cal.loss_evals += X0.shape[0] * (N_PARAMS + 1)
+        surf.fg_begin(X0, cal.spot, cal.risk_free_rate, cal.N, model=model, slot=k)
+        inflight[k] = ids
+
+    submit(0)
+    submit(1)
+    while inflight[0] is not None or inflight[1] is not None:
+        for k in (0, 1):
+            ids = inflight[k]
+            if ids is None:
+                continue
+            f0, G, lows = surf.fg_end(k)
+            launches += 1
+            _consume(states, gens, pending, outcomes, ids, f0, G, lows)
+            submit(k)
     cal.lockstep_launches = launches
 
 

@@ -338,19 +338,51 @@ def test_robust_start_matches_reference_exactly(dh, calib_golden):
 
 
 def test_lockstep_equals_sequential(dh, calib_golden):
-    """Lockstep batching (3 starts x 14 sets per launch) is bitwise identical to running the
-    starts one after another: each start's values depend only on its own x."""
+    """Lockstep batching (3 starts x 14 sets per launch), the two-group pipeline (starts 0, 2 and
+    start 1 alternating on the device, dh_surface_fg_begin / _end) and running the starts one
+    after another are bitwise identical: each start's values depend only on its own x."""
     g = calib_golden
     from dhcos.calibrator import run_starts
     cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
     x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
-    a = run_starts(cal, x0s, 300, lockstep=True)
+    a = run_starts(cal, x0s, 300, lockstep=True, pipeline=False)
     launches = cal.lockstep_launches
+    p = run_starts(cal, x0s, 300, lockstep=True)
+    p_launches = cal.lockstep_launches
     b = run_starts(cal, x0s, 300, lockstep=False)
-    for (ra, _), (rb, _) in zip(a, b):
-        assert np.array_equal(ra.x, rb.x) and ra.fun == rb.fun and ra.nit == rb.nit
-        assert ra.message == rb.message
-    assert launches == max(r.nfev for r, _ in a)   # one launch per lockstep round
+    for (ra, _), (rp, _), (rb, _) in zip(a, p, b):
+        for r in (rp, rb):
+            assert np.array_equal(ra.x, r.x) and ra.fun == r.fun and ra.nit == r.nit
+            assert ra.message == r.message and ra.nfev == r.nfev
+    nfev = [r.nfev for r, _ in a]
+    assert launches == max(nfev)                       # one launch per lockstep round
+    assert p_launches == max(nfev[0::2]) + max(nfev[1::2])   # one per group round
+
+
+def test_fg_begin_end_slots(dh, calib_golden):
+    """The asynchronous halves of dh_surface_fg: two requests in flight (one per slot) give
+    fg's bits; a busy slot, an empty slot and a bad slot index are errors."""
+    from dhcos import _native
+    from dhcos.calibrator import fd_models
+    g = calib_golden
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    surf = cal._get_surface()
+    X = np.array([s["x0"] for s in g["calibrate_seed0_starts"]], dtype=float)
+    A, B = X[:2], X[2:]
+    surf.fg_begin(A, 100.0, 0.05, 128, model=fd_models(A), slot=0)
+    with pytest.raises(_native.NativeError):
+        surf.fg_begin(A, 100.0, 0.05, 128, model=fd_models(A), slot=0)
+    surf.fg_begin(B, 100.0, 0.05, 128, model=fd_models(B), slot=1)
+    fb = surf.fg_end(1)
+    fa = surf.fg_end(0)
+    with pytest.raises(_native.NativeError):
+        surf.fg_end(0)
+    with pytest.raises(_native.NativeError):
+        surf.fg_begin(A, 100.0, 0.05, 128, slot=2)
+    for got, Xi in ((fa, A), (fb, B)):
+        want = surf.fg(Xi, 100.0, 0.05, 128, model=fd_models(Xi))
+        for u, v in zip(got, want):
+            assert np.array_equal(u, v)
 
 
 def test_generator_matches_reference(dh, gen_golden, tmp_path):
