@@ -246,6 +246,8 @@ int dh_comm_create(dh_ctx* ctx, const unsigned char* id, int world, int rank, dh
 int dh_comm_destroy(dh_comm* comm);
 /* buf[n] (host): root's values on every rank (the start x0s and the RNG state after the draws). */
 int dh_comm_broadcast(dh_comm* comm, double* buf, int64_t n, int root);
+/* send[n] (host) of every rank -> recv[world][n] in rank order (the generator's price blocks). */
+int dh_comm_allgather(dh_comm* comm, const double* send, int64_t n, double* recv);
 /* All-gather of fixed-size per-start records: each rank passes rows x width doubles (its starts;
  * rows must be equal on every rank, padding rows carry a negative start index), all receives
  * [world * rows][width] in rank order, and best the winning start index (or -1): the first start,

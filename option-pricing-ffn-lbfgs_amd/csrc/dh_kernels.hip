@@ -3441,6 +3441,23 @@ extern "C" int dh_comm_broadcast(dh_comm* c, double* buf, int64_t n, int root) {
     return DH_OK;
 }
 
+extern "C" int dh_comm_allgather(dh_comm* c, const double* send, int64_t n, double* recv) {
+    if (!c || (n > 0 && (!send || !recv))) return fail(DH_E_ARG, "null argument");
+    if (n < 0) return fail(DH_E_ARG, "n < 0");
+    if (n == 0) return DH_OK;
+    DeviceScope dev_scope(c->ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
+    hipStream_t st = c->ctx->stream;
+    const size_t bytes = (size_t)n * sizeof(double);
+    HIP_TRY(c->send.reserve(bytes));
+    HIP_TRY(c->recv.reserve(bytes * c->world));
+    HIP_TRY(hipMemcpyAsync(c->send.ptr, send, bytes, hipMemcpyHostToDevice, st));
+    NCCL_TRY(rccl().all_gather(c->send.ptr, c->recv.ptr, (size_t)n, ncclFloat64, c->comm, st));
+    HIP_TRY(hipMemcpyAsync(recv, c->recv.ptr, bytes * c->world, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return DH_OK;
+}
+
 extern "C" int dh_best_start(const double* all, int64_t rows, int width, int col_start,
                              int col_fun, int* best) {
     if (!best || (rows > 0 && !all)) return fail(DH_E_ARG, "null argument");
@@ -3470,18 +3487,7 @@ extern "C" int dh_allgather_best(dh_comm* c, const double* rec, int rows, int wi
                                  int col_start, int col_fun, double* all, int* best) {
     if (!c || !all || !best || (rows > 0 && !rec)) return fail(DH_E_ARG, "null argument");
     if (rows < 0 || width < 1) return fail(DH_E_ARG, "rows / width out of range");
-    const size_t per = (size_t)rows * width;
-    if (per > 0) {
-        DeviceScope dev_scope(c->ctx->device);
-        if (dev_scope.rc) return dev_scope.rc;
-        hipStream_t st = c->ctx->stream;
-        HIP_TRY(c->send.reserve(per * sizeof(double)));
-        HIP_TRY(c->recv.reserve(per * c->world * sizeof(double)));
-        HIP_TRY(hipMemcpyAsync(c->send.ptr, rec, per * sizeof(double), hipMemcpyHostToDevice, st));
-        NCCL_TRY(rccl().all_gather(c->send.ptr, c->recv.ptr, per, ncclFloat64, c->comm, st));
-        HIP_TRY(hipMemcpyAsync(all, c->recv.ptr, per * c->world * sizeof(double),
-                               hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-    }
+    const int rc = dh_comm_allgather(c, rec, (int64_t)rows * width, all);
+    if (rc) return rc;
     return dh_best_start(all, (int64_t)rows * c->world, width, col_start, col_fun, best);
 }

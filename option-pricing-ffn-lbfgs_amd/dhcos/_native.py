@@ -99,6 +99,7 @@ SIGNATURES = {
     "dh_comm_destroy": (C.c_int, [_vp]),
     "dh_comm_broadcast": (C.c_int, [_vp, _vp, C.c_int64, C.c_int]),
     "dh_allgather_best": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _i32p]),
+    "dh_comm_allgather": (C.c_int, [_vp, _vp, C.c_int64, _vp]),
     "dh_best_start": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.c_int, _i32p]),
 }
 
@@ -497,6 +498,14 @@ class Comm:
         out = np.ascontiguousarray(buf, dtype=np.float64)
         _check(load().dh_comm_broadcast(self._h, out.ctypes.data if out.size else None, out.size,
                                         int(root)))
+        return out
+
+    def allgather(self, block) -> np.ndarray:
+        """block (float64, same size on every rank) -> [world, *block.shape] in rank order."""
+        blk = np.ascontiguousarray(block, dtype=np.float64)
+        out = np.empty((self.world,) + blk.shape)
+        _check(load().dh_comm_allgather(self._h, blk.ctypes.data if blk.size else None, blk.size,
+                                        out.ctypes.data if out.size else None))
         return out
 
     def allgather_best(self, records, col_start: int, col_fun: int):

@@ -222,12 +222,12 @@ def sample_block(n: int, rank: int, world: int):
 def generate_sharded(n_samples: int = 500,
                      save_path: str = "lbfgs_calibrations_synthetic.pkl", *, N: int = 128,
                      as_arrays: bool = False, verbose: bool = True, group=None, price_fn=None,
-                     device=None):
+                     device=None, comm=None):
     """``generate_synthetic_calibrations`` with the pricing sharded over the process group.
     Rank 0 returns (and saves) the reference output; other ranks return None."""
     from . import generator as G
 
-    rank, world = _world(group)
+    rank, world = _world(group, comm)
     price_fn = price_fn or (lambda p, s: G.price_grid(p, s, N=N, device=device))
     n_opt = len(G.STRIKES_PCT) * len(G.MATURITIES)
     width = 13 + 1 + n_opt
@@ -236,22 +236,25 @@ def generate_sharded(n_samples: int = 500,
         params, spots, noise = G.draw_paths(n_samples)
         draws = np.concatenate([np.concatenate([params, spots[:, None], noise], axis=1).ravel(),
                                 _rng_state_vec()])
-    if world > 1:
-        draws = _broadcast_f64(draws, (n_samples * width + 627,), group, device)
+    if world > 1 or comm is not None:
+        draws = _broadcast_f64(draws, (n_samples * width + 627,), group, device, comm)
         _set_rng_state_vec(draws[n_samples * width:])
     draws = draws[:n_samples * width].reshape(n_samples, width)
     params, spots, noise = draws[:, :13], draws[:, 13], draws[:, 14:]
     lo, hi = sample_block(n_samples, rank, world)
     block = price_fn(params[lo:hi], spots[lo:hi]) if hi > lo else np.empty((0, n_opt))
-    if world > 1:
+    if world > 1 or comm is not None:
         per = (n_samples + world - 1) // world
         buf = np.zeros((per, n_opt))
         buf[:hi - lo] = block
-        dev = _comm_device(group, device)
-        mine = torch.from_numpy(buf).to(dev)
-        parts = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(parts, mine, group=group)
-        model = np.concatenate([p.cpu().numpy() for p in parts])[:n_samples]
+        if comm is not None:
+            model = comm.allgather(buf).reshape(world * per, n_opt)[:n_samples]
+        else:
+            dev = _comm_device(group, device)
+            mine = torch.from_numpy(buf).to(dev)
+            parts = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine, group=group)
+            model = np.concatenate([p.cpu().numpy() for p in parts])[:n_samples]
     else:
         model = block
     if rank != 0:

@@ -53,3 +53,22 @@ def test_calibrate_sharded_over_native_comm_equals_calibrate(comm, calib_golden)
     assert got.message == w.message and got.parameters == w.parameters
     np.testing.assert_array_equal(got.model_prices, w.model_prices)
     assert (cal.n_calls, cal.best_loss) == (want.n_calls, want.best_loss)
+
+
+def test_generate_sharded_over_native_comm_equals_generator(comm, tmp_path):
+    """generate_sharded through dh_comm_broadcast / dh_comm_allgather: the generator's output and
+    its np.random continuation."""
+    from dhcos import distributed as D
+    from dhcos import generator as G
+    np.random.seed(5)
+    want = G.generate_synthetic_calibrations(48, str(tmp_path / "a.pkl"), N=64, as_arrays=True,
+                                             verbose=False)
+    after = np.random.rand()
+    np.random.seed(5)
+    got = D.generate_sharded(48, str(tmp_path / "b.pkl"), N=64, as_arrays=True, verbose=False,
+                             comm=comm)
+    assert np.random.rand() == after
+    assert set(got) == set(want)
+    for k in want:
+        a, b = np.asarray(want[k]), np.asarray(got[k])
+        assert a.shape == b.shape and (a == b).all() or np.array_equal(a, b, equal_nan=True), k
