@@ -107,6 +107,8 @@ struct PriceArgs {
     unsigned long long* stamps;   // diagnostic builds (DH_STAMPS) only: [blocks][kStamps]
     const int* live_count;  // device-resident calibration: the launch is a no-op once every start
                             // has finished (*live_count == 0), else null
+    const double* pre;      // fused kernel on large grids: [tables][kTabC] prologue constants
+                            // formed by table_prologue_kernel ahead of it, else null
 };
 
 // A launch enqueued ahead by dh_calibrate_lbfgs after its starts have all finished returns at
@@ -280,6 +282,17 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, int64_t 
         c[27] = gr.x;
         c[28] = gr.y;
     }
+}
+
+// Every table's prologue of a large fused request, one lane per table, ahead of the fused
+// launch (launch_fused): the fused blocks then load their constants instead of running the
+// one-wave prologue chain while their other waves wait at the barrier (C3: 12k of a block's 47k
+// cycles with four blocks per CU).  table_prologue, so the bits of every other path.
+__global__ __launch_bounds__(kBlock) void table_prologue_kernel(PriceArgs A, int64_t n_q,
+                                                                double* out) {
+    if (halted(A)) return;
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q < n_q) table_prologue(A, q, out + q * kTabC);
 }
 
 #ifndef DH_TABLE_WAVES
@@ -1204,7 +1217,11 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(PriceArgs A, int 
 
     // ---- prologue (wave 0, lane-parallel) || per-option staging (wave 0 takes the last
     //      indices) ----
-    if (wv == 0) table_prologue_wave(A, q, shc, lane);
+    if (A.pre) {
+        if (t < kTabC) shc[t] = A.pre[q * kTabC + t];
+    } else if (wv == 0) {
+        table_prologue_wave(A, q, shc, lane);
+    }
     DH_STAMP(A, 8);
     dh::load_math_tables(sct, nthr > 64 ? 64 : 0);      // the waves after the prologue's
     for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
@@ -1573,7 +1590,7 @@ struct dh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf params, out, sse, bad, part_sse, part_bad, counter, exact_prices, table, consts, cl_mask,
-        cl_price, aux0, aux1, aux2, aux3;
+        cl_price, aux0, aux1, aux2, aux3, pre;
     HostBuf h_params, h_loss;  // zero-copy inputs / outputs of small host-API loss requests
     HostBuf h_pairs;           // zero-copy inputs / outputs of small dh_price_pairs calls
     DevBuf lb_state, lb_rec, lb_sse, lb_bad, lb_live, lb_done, lb_x0;   // dh_calibrate_lbfgs
@@ -1729,6 +1746,12 @@ size_t fused_lds_bytes(int N, int cap) {
 #define DH_FUSED_WIDE_MIN_BLOCKS 4096
 #endif
 constexpr int64_t kFusedWideMinBlocks = DH_FUSED_WIDE_MIN_BLOCKS;
+// fused grids from this size take their prologue constants from table_prologue_kernel (C4's
+// 28,672 blocks: 297 -> 285 us; C3's 4,200 lose 3% to the extra launch, C2's 448 its latency)
+#ifndef DH_PROLOGUE_KERNEL_MIN_BLOCKS
+#define DH_PROLOGUE_KERNEL_MIN_BLOCKS 8192
+#endif
+constexpr int64_t kPrologueKernelMinBlocks = DH_PROLOGUE_KERNEL_MIN_BLOCKS;
 
 // One fused launch for the whole request (every group is one tile).
 int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
@@ -1751,6 +1774,13 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     }
     const dim3 grid((unsigned)blocks), block((unsigned)std::max(t1, t2));
     const bool r1 = tile_r(max_nopt, t2) == 1;
+    if (blocks >= kPrologueKernelMinBlocks && !ctx->stamps_on) {
+        HIP_TRY(ctx->pre.reserve((size_t)blocks * kTabC * sizeof(double)));
+        A.pre = (const double*)ctx->pre.ptr;
+        hipLaunchKernelGGL(table_prologue_kernel, dim3((unsigned)((blocks + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, st, A, blocks, (double*)ctx->pre.ptr);
+        HIP_TRY(hipGetLastError());
+    }
     // grids of many small blocks (C4: 28,672) gain from a fifth wave per SIMD to overlap the
     // blocks' latency-bound phases; small grids keep the 4-wave build, whose blocks are shorter
     // (same arithmetic: only the register allocation differs, so the same bits)
@@ -1937,7 +1967,7 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     for (DevBuf* b : {&ctx->params, &ctx->out, &ctx->sse, &ctx->bad, &ctx->part_sse,
                       &ctx->part_bad, &ctx->counter, &ctx->exact_prices, &ctx->stamps, &ctx->table,
                       &ctx->consts, &ctx->cl_mask, &ctx->cl_price, &ctx->aux0,
-                      &ctx->aux1, &ctx->aux2, &ctx->aux3, &ctx->lb_state, &ctx->lb_rec,
+                      &ctx->aux1, &ctx->aux2, &ctx->aux3, &ctx->pre, &ctx->lb_state, &ctx->lb_rec,
                       &ctx->lb_sse, &ctx->lb_bad, &ctx->lb_live, &ctx->lb_done, &ctx->lb_x0,
                       &ctx->lb_trace, &ctx->lb_trace_n})
         b->release();

@@ -538,6 +538,8 @@ def _with_path(ctx, path, fn):
     (48, 192, 1024, 32, 256),    # 6,144 tables: the split path's table kernel takes one-wave
                                  # slots (the smaller cases take 128/256-thread slots), and the
                                  # fused path its 5-wave build (grids of >= 4,096 blocks)
+    (49, 288, 1024, 32, 256),    # 9,216 tables: the fused blocks load their prologue constants
+                                 # from table_prologue_kernel (grids of >= 8,192 blocks)
 ])
 def test_fused_equals_split_bitwise(dh, seed, P, M, n_T, N):
     """The fused single-launch request kernel and the table + option launches compute every
