@@ -147,7 +147,7 @@ def cpu_options(cfg):
 def kernel_label(ctx):
     """Kernels of the last request on ctx (after the bench's own launches)."""
     if ctx.last_path == _native.PATH_FUSED:
-        return "cos_fused_kernel"
+        return "cos_fused_kernel (after table_prologue_kernel on grids of >= 8,192 tables)"
     return "cos_table_kernel + cos_option[_small]_kernel"
 
 

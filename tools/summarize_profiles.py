@@ -23,7 +23,8 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel")
+KERNELS = ("cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel",
+           "table_prologue_kernel")
 
 
 def short(name):
@@ -50,7 +51,8 @@ def main():
     tpath = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     md = [f"# Profile summary {args.tag}", "",
-          "One request = cos_fused_kernel (every maturity group one tile: C1-C4), or "
+          "One request = cos_fused_kernel (every maturity group one tile: C1-C4; on grids of "
+          ">= 8,192 blocks, C4, preceded by table_prologue_kernel), or "
           "cos_table_kernel + the option kernel (cos_option_kernel for multi-tile groups, "
           "cos_option_small_kernel for large calls on <=16-option tiles: C5). Durations: "
           "rocprofv3 --kernel-trace --stats average; counters: per-launch medians of separate "
@@ -76,9 +78,11 @@ def main():
         # table kernel + whichever option-kernel variant dominates (the others only serve the
         # bench's small spot-check calls)
         if total.get("cos_fused_kernel", 0.0) >= max(total.values()):
-            req_kernels = ("cos_fused_kernel",)
+            # large fused grids run table_prologue_kernel ahead of the fused kernel
+            pro = total.get("table_prologue_kernel", 0.0) >= 0.01 * total["cos_fused_kernel"]
+            req_kernels = (("table_prologue_kernel",) if pro else ()) + ("cos_fused_kernel",)
         else:
-            opt = max((k for k in KERNELS[2:] if k in total), key=lambda k: total[k])
+            opt = max((k for k in KERNELS[2:4] if k in total), key=lambda k: total[k])
             req_kernels = ("cos_table_kernel", opt)
         vals = collections.defaultdict(list)
         for f in glob.glob(os.path.join(args.src, f"{args.tag}_{c}_pmc*_counter_collection.csv")):
