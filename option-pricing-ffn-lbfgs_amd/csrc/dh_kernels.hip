@@ -1597,6 +1597,7 @@ struct dh_ctx {
     HostBuf h_lb;              // finished flags / live list of dh_calibrate_lbfgs
     // the two in-flight slots of dh_surface_fg_begin / _end: zero-copy records in, sse / n_bad
     // out, the host-side Feller terms and FD steps, and the request's completion event
+    size_t fg_max_units = 0;   // largest (param sets x tasks) of any dh_surface_fg_begin request
     struct FgSlot {
         HostBuf h_params, h_loss;
         std::vector<double> pen, dx;
@@ -3285,12 +3286,13 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
         return fail(DH_E_ARG, "too many starts for one asynchronous request (use dh_surface_fg)");
     DeviceScope dev_scope(ctx->device);
     if (dev_scope.rc) return dev_scope.rc;
-    // the loss launch grows the context's device scratch when this request is larger than any
-    // before; a grow frees the old buffers, so let the other slot's request finish first
+    // the loss launch grows the context's device scratch (partials, counters, the prologue
+    // buffer, clamp workspaces) when this request has more tasks than any before; a grow frees
+    // the old buffers, so let the other slot's request finish first
     auto& O = ctx->fg[1 - slot];
-    if (O.pending && (P * s->n_tiles * 8 > ctx->part_sse.cap ||
-                      P * kCounterStride * 4 > ctx->counter.cap))
-        HIP_TRY(hipEventSynchronize(O.done));
+    const size_t units = P * (size_t)std::max(s->n_tiles, s->n_groups);
+    if (O.pending && units > ctx->fg_max_units) HIP_TRY(hipEventSynchronize(O.done));
+    ctx->fg_max_units = std::max(ctx->fg_max_units, units);
     HIP_TRY(F.h_params.reserve(P * DH_PARAM_STRIDE * 8));
     HIP_TRY(F.h_loss.reserve(P * 12));
     F.pen.resize(P);
