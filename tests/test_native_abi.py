@@ -78,3 +78,22 @@ def test_null_and_range_arguments_are_rejected():
     lib.dh_device_count(C.byref(n))
     assert n.value >= 0
     assert np.int8(1) == 1
+
+
+def test_comm_and_async_fg_arguments_are_rejected():
+    """The communicator and the two-slot FD request validate their arguments before any device or
+    RCCL work."""
+    import ctypes as C
+    from dhcos import _native
+    lib = _native.load()
+    out = C.c_void_p()
+    uid = C.create_string_buffer(_native.COMM_ID_BYTES)
+    assert lib.dh_comm_create(None, C.cast(uid, C.c_void_p), 1, 0, C.byref(out)) == -1
+    assert lib.dh_comm_destroy(None) == 0
+    assert lib.dh_comm_broadcast(None, None, 4, 0) == -1
+    assert lib.dh_comm_allgather(None, None, 4, None) == -1
+    best = C.c_int32(7)
+    assert lib.dh_allgather_best(None, None, 1, 3, 0, 1, None, C.byref(best)) == -1
+    assert lib.dh_surface_fg_begin(None, None, None, None, 1, 100.0, 0.05, 128, 10.0, 0) == -1
+    assert lib.dh_surface_fg_end(None, None, 0, None, None, None) == -1
+    assert b"null" in lib.dh_last_error()
