@@ -100,7 +100,9 @@ struct PriceArgs {
     unsigned* counter;      // [P * kCounterStride] arrival counters (zero between launches)
     double* sse;            // [P] final sums (loss mode)
     int* n_bad;             // [P]
-    double* table;          // workspace: [np*tabs_per_p][N] = w_k
+    double* table;          // workspace: w_k, [np*tabs_per_p][N], or tiled (table_tiled) as
+                            // [np*tabs_per_p / kTabTile][N][kTabTile]
+    int table_tiled;        // set when cos_option_small_kernel reads the tables (table_w)
     double* consts;         // workspace: [np*tabs_per_p][kConsts]
     unsigned long long* cl_mask;   // workspace: [np*tabs_per_p][cl_words] clamp bits per option
     double* cl_price;       // workspace: [np*tabs_per_p][max_group] prices of clamped options
@@ -110,6 +112,18 @@ struct PriceArgs {
     const double* pre;      // fused kernel on large grids: [tables][kTabC] prologue constants
                             // formed by table_prologue_kernel ahead of it, else null
 };
+
+// w_k of table q sits at table_w(A, q)[k * table_step(A)].  The small-tile option kernel has one
+// lane per table, so a row-major table puts every lane of a load on its own line (64 lines per
+// wave-load, ~30% VALU issue in round 2); tiled, kTabTile consecutive tables share each line and
+// a wave-load touches 4 lines.  The table kernel's writes then scatter over kTabTile-table lines
+// that its 64-table batches fill within L2.
+constexpr int kTabTile = 16;
+__device__ __forceinline__ int table_step(const PriceArgs& A) { return A.table_tiled ? kTabTile : 1; }
+__device__ __forceinline__ double* table_w(const PriceArgs& A, int64_t q) {
+    return A.table_tiled ? A.table + (q / kTabTile) * kTabTile * (int64_t)A.N + (q % kTabTile)
+                         : A.table + q * (int64_t)A.N;
+}
 
 // A launch enqueued ahead by dh_calibrate_lbfgs after its starts have all finished returns at
 // once.  The count only changes between launches (the step kernel writes it), so every block of
@@ -375,9 +389,10 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                     double* cc = (double*)&CC;
                     for (int j = 0; j < 16; ++j) cc[j] = c[6 + j];
                 }
-                double* tw = A.table + q * (int64_t)N;
+                double* tw = table_w(A, q);
+                const int ts = table_step(A);
                 table_entries<TPT>(CC, t, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
-                    tw[k] = w;
+                    tw[k * ts] = w;
                     if (k == 0) {
                         w0 = 0.5 * w;
                         return;
@@ -930,7 +945,7 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     // kernel's k-sums), and per-option data: log(K/S0), e^{xK} and the G-step rotation of each
     // option; clamp-widened options (bit set by the table kernel) are recorded right here
     if (active) {
-        const double* tw = A.table + q * (int64_t)N;
+        const double* tw = A.table + q * (int64_t)N;     // row-major (never tiled here)
         const double piba = dh::kPi / ba;
         for (int k = t; k < N; k += TPT) {
             const double w = tw[k];
@@ -1076,7 +1091,8 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
         sp[j] = 0.0;
         sm[j] = 0.0;
     }
-    const double* tw = A.table + q * (int64_t)A.N;
+    // the host always tiles the tables this kernel reads: entry k at tw[k * kTabTile]
+    const double* tw = A.table + (q / kTabTile) * kTabTile * (int64_t)A.N + (q % kTabTile);
     double c2[RS];
 #pragma unroll
     for (int j = 0; j < RS; ++j) c2[j] = 2.0 * cs[j];
@@ -1095,15 +1111,15 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
         }
         const int kend = min(N, k0 + kAnchor);
         int k = k0;
-        double wa = active ? tw[k] : 0.0;
+        double wa = active ? tw[k * kTabTile] : 0.0;
         for (; k + 1 < kend; k += 2) {
-            const double wb = active ? tw[k + 1] : 0.0;
+            const double wb = active ? tw[(k + 1) * kTabTile] : 0.0;
             const double ua = k * piba, ub = (k + 1) * piba;
             const double T2a = wa * S0 * dh::drcp(1.0 + ua * ua);
             const double T6a = -(T2a * dh::drcp(ua));
             const double T2b = wb * S0 * dh::drcp(1.0 + ub * ub);
             const double T6b = -(T2b * dh::drcp(ub));
-            wa = active ? tw[min(k + 2, N - 1)] : 0.0;
+            wa = active ? tw[min(k + 2, N - 1) * kTabTile] : 0.0;
 #pragma unroll
             for (int j = 0; j < RS; ++j) {
                 sm[j] = fma(T2a, c[j], sm[j]);
@@ -1834,7 +1850,9 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     const size_t per_p =
         (size_t)tpp * ((size_t)N + kConsts + words + (size_t)A0.max_group) * sizeof(double);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A0.P, kTableBudget / per_p));
-    HIP_TRY(ctx->table.reserve((size_t)chunk * tpp * N * sizeof(double)));
+    // rounded up to whole kTabTile-table tiles (the small-tile kernel's layout)
+    HIP_TRY(ctx->table.reserve((size_t)((chunk * tpp + kTabTile - 1) / kTabTile) * kTabTile * N *
+                               sizeof(double)));
     HIP_TRY(ctx->consts.reserve((size_t)chunk * tpp * kConsts * sizeof(double)));
     HIP_TRY(ctx->cl_mask.reserve((size_t)chunk * tpp * words * 8));
     HIP_TRY(ctx->cl_price.reserve((size_t)chunk * tpp * A0.max_group * sizeof(double)));
@@ -1872,6 +1890,7 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         A.p0 = p0;
         A.np = std::min<int64_t>(chunk, A0.P - p0);
         A.table = (double*)ctx->table.ptr;
+        A.table_tiled = small ? 1 : 0;
         A.consts = (double*)ctx->consts.ptr;
         A.cl_mask = (unsigned long long*)ctx->cl_mask.ptr;
         A.cl_price = (double*)ctx->cl_price.ptr;
