@@ -241,16 +241,35 @@ __device__ __forceinline__ double lane_bcast(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-__device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, int64_t q, double* c,
-                                                    int lane) {
+// The fused kernel's leading arguments: what its prologue reads first.  As plain scalar kernel
+// arguments ahead of PriceArgs they are preloaded into SGPRs at wave launch (gfx950 kernarg
+// preloading, -mllvm -amdgpu-kernarg-preload-count, Makefile), so the parameter, maturity and
+// group loads issue at once instead of behind a kernel-argument load (one memory round trip
+// less on the request's critical path).  The fused launch has p0 = 0.
+struct FusedHead {
+    const double* prm;      // PriceArgs::prm
+    const double* tsrc;     // PriceArgs::T (paired) or ::group_T
+    const int2* groups;     // PriceArgs::groups
+    const int* live;        // PriceArgs::live_count, or kLiveOne when null
+    const double* pre;      // PriceArgs::pre
+    int tpp;                // tabs_per_p
+    int paired;
+};
+
+// the live count read by launches without one (FusedHead::live): the halt test is then a load
+// like any other, with no branch on the pointer (a branch made the compiler wait for it at the
+// kernel's entry)
+__device__ const int kLiveOne = 1;
+
+__device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const FusedHead& H,
+                                                    int64_t q, double* c, int lane) {
 #pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
-    const int tpp = tabs_per_p(A);
-    const int64_t p = A.p0 + q / tpp;
-    const int g = (int)(q % tpp);
-    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
-    const double T = A.paired ? A.T[p] : A.group_T[g];
+    const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
+    const int g = (int)((unsigned)q % (unsigned)H.tpp);
+    const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
+    const double T = H.tsrc[H.paired ? p : g];
     int2 gr = make_int2((int)p, 1);
-    if (!A.paired) gr = A.groups[g];
+    if (!H.paired) gr = H.groups[g];
     const bool two = lane & 1;                     // factor 2 on odd lanes
     const double v0 = two ? P.v02 : P.v01, k = two ? P.k2 : P.k1, th = two ? P.t2 : P.t1;
     const double sg = two ? P.s2 : P.s1, rh = two ? P.r2 : P.r1;
@@ -1197,10 +1216,16 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, i
 // cos_option_kernel<tpt2>, so the two paths give the same bits.
 // ----------------------------------------------------------------------------------------------
 template <int TPT1, int RT, int WV = DH_FUSED_WAVES>
-__global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(PriceArgs A, int tpt2) {
-    // the halt test waits on a global load: taken after the staging barrier, so the load
-    // overlaps the prologue instead of delaying it (a halted launch wastes the prologue only)
-    const bool halt = halted(A);
+__global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
+    const double* __restrict__ h_prm, const double* __restrict__ h_tsrc,
+    const int2* __restrict__ h_groups, const int* __restrict__ h_live,
+    const double* __restrict__ h_pre, int h_tpp, int h_paired, PriceArgs A, int tpt2) {
+    const FusedHead H{h_prm, h_tsrc, h_groups, h_live ? h_live : &kLiveOne, h_pre, h_tpp,
+                      h_paired};
+    // the halt test's load is issued here (a global load: a flat one would also hold up every
+    // scalar load's wait) and its value used after the staging barrier, so it overlaps the
+    // prologue instead of delaying it (a halted launch wastes the prologue only)
+    const int live_v = *(const __attribute__((address_space(1))) int*)H.live;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ double shc[kTabC];
     __shared__ double red[4][1];
@@ -1210,35 +1235,35 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(PriceArgs A, int 
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wv = t >> 6;
-    const int N = A.N;
-    const int tpp = tabs_per_p(A);
     const int64_t q = blockIdx.x;
-    const int64_t p = A.p0 + q / tpp;
-    const int g = (int)(q % tpp);
+    const int64_t p = (int64_t)(blockIdx.x / (unsigned)H.tpp);    // 32-bit: grids < 2^31 blocks
+    const int g = (int)(blockIdx.x % (unsigned)H.tpp);
+    DH_STAMP(A, 0);
+
+    // ---- prologue (wave 0, lane-parallel) || per-option staging (wave 0 takes the last
+    //      indices).  The prologue comes first in program order and reads the preloaded
+    //      arguments only, so its loads issue before any kernel-argument wait ----
+    if (H.pre) {
+        if (t < kTabC) shc[t] = H.pre[q * kTabC + t];
+    } else if (wv == 0) {
+        table_prologue_wave(A, H, q, shc, lane);
+    }
+    DH_STAMP(A, 8);
+    const int N = A.N;
     const int cap = A.opt_cap;
     const TileLds L = tile_lds(smem, N, cap);
     double* lclp = smem + option_lds_doubles(N, cap);     // prices of clamp-widened options
     int g0, gn;
-    if (A.paired) {
+    if (H.paired) {
         g0 = (int)p;
         gn = 1;
     } else {
-        const int2 gr = A.groups[g];
+        const int2 gr = H.groups[g];
         g0 = gr.x;
         gn = gr.y;
     }
-    const double* prm = A.prm + p * DH_PARAM_STRIDE;
+    const double* prm = H.prm + p * DH_PARAM_STRIDE;
     const double S0 = prm[13];
-    DH_STAMP(A, 0);
-
-    // ---- prologue (wave 0, lane-parallel) || per-option staging (wave 0 takes the last
-    //      indices) ----
-    if (A.pre) {
-        if (t < kTabC) shc[t] = A.pre[q * kTabC + t];
-    } else if (wv == 0) {
-        table_prologue_wave(A, q, shc, lane);
-    }
-    DH_STAMP(A, 8);
     dh::load_math_tables(sct, nthr > 64 ? 64 : 0);      // the waves after the prologue's
     for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
         const int m = g0 + i;
@@ -1253,7 +1278,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(PriceArgs A, int 
         L.exK[i] = ratio;
     }
     __syncthreads();
-    if (halt) return;                              // uniform: every block reads the same count
+    if (__builtin_amdgcn_readfirstlane(live_v) <= 0) return;   // every block reads the same count
     DH_STAMP(A, 1);
 
     const double a = shc[0], b = shc[1], eb = shc[2], ea = shc[3], scale = shc[4], piba = shc[5];
@@ -1790,6 +1815,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         A.stamps = (unsigned long long*)ctx->stamps.ptr;
     }
     const dim3 grid((unsigned)blocks), block((unsigned)std::max(t1, t2));
+    const double* tsrc = A.paired ? A.T : A.group_T;       // FusedHead: preloaded arguments
     const bool r1 = tile_r(max_nopt, t2) == 1;
     if (blocks >= kPrologueKernelMinBlocks && !ctx->stamps_on) {
         HIP_TRY(ctx->pre.reserve((size_t)blocks * kTabC * sizeof(double)));
@@ -1803,20 +1829,20 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     // (same arithmetic: only the register allocation differs, so the same bits)
     if (r1 && blocks >= kFusedWideMinBlocks) {
         switch (t1) {
-            case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A, t2); break;
-            case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A, t2); break;
-            default: hipLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A, t2); break;
+            case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+            case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+            default: hipLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
         }
         HIP_TRY(hipGetLastError());
         return DH_OK;
     }
     switch (t1 * (r1 ? 1 : -1)) {
-        case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1>), grid, block, lds, st, A, t2); break;
-        case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1>), grid, block, lds, st, A, t2); break;
-        case 256: hipLaunchKernelGGL((cos_fused_kernel<256, 1>), grid, block, lds, st, A, t2); break;
-        case -64: hipLaunchKernelGGL((cos_fused_kernel<64, kR>), grid, block, lds, st, A, t2); break;
-        case -128: hipLaunchKernelGGL((cos_fused_kernel<128, kR>), grid, block, lds, st, A, t2); break;
-        default: hipLaunchKernelGGL((cos_fused_kernel<256, kR>), grid, block, lds, st, A, t2); break;
+        case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+        case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+        case 256: hipLaunchKernelGGL((cos_fused_kernel<256, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+        case -64: hipLaunchKernelGGL((cos_fused_kernel<64, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+        case -128: hipLaunchKernelGGL((cos_fused_kernel<128, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+        default: hipLaunchKernelGGL((cos_fused_kernel<256, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
     }
     HIP_TRY(hipGetLastError());
     return DH_OK;
