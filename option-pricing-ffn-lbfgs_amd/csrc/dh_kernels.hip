@@ -256,6 +256,20 @@ struct FusedHead {
     int paired;
 };
 
+// A by-value kernel argument read in place: its fields load from the kernel-argument segment at
+// their uses.  (Every use of a by-value argument is lowered to a load in the kernel's entry block;
+// with the SGPR file full the compiler then spills them to VGPR lanes at once, which waits for the
+// whole load before the prologue's first memory access can issue.)  off = the argument's byte
+// offset in the segment: the preceding arguments at their natural alignment.
+template <typename T, int off>
+__device__ __forceinline__ const T& karg_ref() {
+    typedef const __attribute__((address_space(4))) char* KargPtr;
+    const KargPtr k = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    return *(const T*)(const char*)(k + off);
+}
+// FusedHead's arguments: 5 pointers and 2 ints, so PriceArgs starts at byte 48
+constexpr int kFusedArgsKernargOff = 48;
+
 // the live count read by launches without one (FusedHead::live): the halt test is then a load
 // like any other, with no branch on the pointer (a branch made the compiler wait for it at the
 // kernel's entry)
@@ -1219,9 +1233,10 @@ template <int TPT1, int RT, int WV = DH_FUSED_WAVES>
 __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const double* __restrict__ h_prm, const double* __restrict__ h_tsrc,
     const int2* __restrict__ h_groups, const int* __restrict__ h_live,
-    const double* __restrict__ h_pre, int h_tpp, int h_paired, PriceArgs A, int tpt2) {
+    const double* __restrict__ h_pre, int h_tpp, int h_paired, PriceArgs A_, int tpt2) {
     const FusedHead H{h_prm, h_tsrc, h_groups, h_live ? h_live : &kLiveOne, h_pre, h_tpp,
                       h_paired};
+    const PriceArgs& A = karg_ref<PriceArgs, kFusedArgsKernargOff>();
     // the halt test's load is issued here (a global load: a flat one would also hold up every
     // scalar load's wait) and its value used after the staging barrier, so it overlaps the
     // prologue instead of delaying it (a halted launch wastes the prologue only)
@@ -2664,12 +2679,22 @@ struct LbArgs {
 };
 static_assert(std::is_standard_layout<LbArgs>::value, "lb_live_inline reads LbArgs by offset");
 
-// live_inline[slot] as a scalar load straight from the kernel-argument segment (LbArgs is the
-// kernel's only argument); indexing the by-value argument compiled to a flat load
+// The step kernel's leading arguments (LbHead), ahead of LbArgs: plain scalars, preloaded into
+// SGPRs at wave launch (Makefile PRELOAD), so the state and partial loads of the load phase issue
+// at once instead of behind a kernel-argument load.  With at most kLbPre live starts their slots'
+// start indices travel here as well (lb_step_kernel<true>).
+constexpr int kLbPre = 4;
+// byte offset of LbArgs in the kernel-argument segment: the leading arguments in declaration order
+// at their natural alignment (2 pointers, 3 + kLbPre ints = 44 bytes), then LbArgs 8-aligned
+constexpr int kLbArgsKernargOff = 48;
+
+// live_inline[slot] as a scalar load straight from the kernel-argument segment; indexing the
+// by-value argument compiled to a flat load
 __device__ __forceinline__ int lb_live_inline(int slot) {
     typedef const __attribute__((address_space(4))) char* KargPtr;
     const KargPtr k = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
-    return ((const __attribute__((address_space(4))) int*)(k + offsetof(LbArgs, live_inline)))
+    return ((const __attribute__((address_space(4))) int*)(k + kLbArgsKernargOff +
+                                                            offsetof(LbArgs, live_inline)))
         [slot < kLbInline ? slot : 0];
 }
 
@@ -2766,15 +2791,23 @@ __device__ __forceinline__ void lb_tile_tree(const double* ps, int nt, double& s
 // pair memory into LDS), consume the finished request (lane t forms loss t, lane i gradient
 // component i), run the L-BFGS-B state machine until it needs a new point, emit that request,
 // store the state.
-__global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
+template <bool kPre>
+__global__ __launch_bounds__(64) void lb_step_kernel(
+    LbSlot* __restrict__ h_states, const double* __restrict__ h_part, int h_ntiles, int h_mode,
+    int h_part_mode, int h_l0, int h_l1, int h_l2, int h_l3, LbArgs A_) {
+    const LbArgs& A = karg_ref<LbArgs, kLbArgsKernargOff>();   // read in place (karg_ref)
     __shared__ double ring[kLbRing + dhlb::kM];
     __shared__ double fl[dhlb::kLanes];
     __shared__ double pb[dhlb::kLanes], pp[dhlb::kLanes];
     [[maybe_unused]] const unsigned long long t_start = lb_clock();
     const int slot = blockIdx.x;
     const int lane = threadIdx.x;
-    const int sidx = A.n_inline ? lb_live_inline(slot) : A.live[slot];
-    LbSlot* G = A.states + sidx;
+    int sidx;
+    if constexpr (kPre)                                // slot < kLbPre (the host's choice)
+        sidx = slot == 0 ? h_l0 : (slot == 1 ? h_l1 : (slot == 2 ? h_l2 : h_l3));
+    else
+        sidx = A.n_inline ? lb_live_inline(slot) : A.live[slot];
+    LbSlot* G = h_states + sidx;
     WaveCore c;
     [[maybe_unused]] unsigned long long t_load = 0, t_req = 0, t_sm = 0;
     c.pairs = WaveRing{ring, ring + dhlb::kM * dhlb::kLanes, ring + 2 * dhlb::kM * dhlb::kLanes,
@@ -2782,7 +2815,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     WaveVec dx, pen;
     double req_sse = 0.0;
     int req_bad = 0;
-    if (A.mode == 0) {
+    if (h_mode == 0) {
         c.s = dhlb::LbScalars{};
         const WaveVec z{0.0};
         c.x = c.g = c.z = c.d = c.t = c.r = c.ge = z;
@@ -2795,7 +2828,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     } else {
         // every load is issued before any is used (one memory round trip): the finished request's
         // loss terms, the pair memory, the vectors and the scalars
-        if (A.mode == 1 && A.part_mode) {
+        if (h_mode == 1 && h_part_mode) {
             // the loss hand-off's sum (task_loss), formed by lane t of every row for point t
             // (lb_tile_tree: the same additions, so the same bits).  Measured alternatives, all
             // slower: staging the request's contiguous partials through LDS with coalesced loads
@@ -2803,13 +2836,13 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
             // state's (5.6k)
             const int li = lane & 15;
             if (li < dhlb::kPts) {
-                const int nt = A.n_tiles;
-                const double* ps = A.part_sse + ((size_t)slot * dhlb::kPts + li) * nt;
+                const int nt = h_ntiles;
+                const double* ps = h_part + ((size_t)slot * dhlb::kPts + li) * nt;
                 if (nt <= 16) lb_tile_tree<16>(ps, nt, req_sse, req_bad);
                 else if (nt <= 32) lb_tile_tree<32>(ps, nt, req_sse, req_bad);
                 else lb_tile_tree<64>(ps, nt, req_sse, req_bad);
             }
-        } else if (A.mode == 1 && (lane & 15) < dhlb::kPts) {
+        } else if (h_mode == 1 && (lane & 15) < dhlb::kPts) {
             const size_t i = (size_t)slot * dhlb::kPts + (lane & 15);
             req_sse = A.sse[i];
             req_bad = A.bad[i];
@@ -2840,7 +2873,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
     }
     int need = 1;
     double* tr = nullptr;                              // this request's trace record, if any
-    if (A.mode == 1) {
+    if (h_mode == 1) {
         t_load = lb_clock();
         double f = __builtin_huge_val();
         if ((lane & 15) < dhlb::kPts) f = req_bad > 0 ? kInvalidLoss : req_sse / (double)A.M + pen.v;
@@ -2870,7 +2903,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
         }
     }
     __syncthreads();
-    if (A.mode == 1) {
+    if (h_mode == 1) {
         t_req = lb_clock();
         need = dhlb::lb_resume(c, A.cfg);
         t_sm = lb_clock();
@@ -2911,7 +2944,15 @@ __global__ __launch_bounds__(64) void lb_step_kernel(LbArgs A) {
 }
 
 int launch_lb_step(hipStream_t st, const LbArgs& A, int n_live) {
-    hipLaunchKernelGGL(lb_step_kernel, dim3((unsigned)n_live), dim3(64), 0, st, A);
+    if (A.n_inline && n_live <= kLbPre) {
+        int l[kLbPre] = {0, 0, 0, 0};
+        for (int i = 0; i < n_live; ++i) l[i] = A.live_inline[i];
+        hipLaunchKernelGGL(lb_step_kernel<true>, dim3((unsigned)n_live), dim3(64), 0, st, A.states,
+                           A.part_sse, A.n_tiles, A.mode, A.part_mode, l[0], l[1], l[2], l[3], A);
+    } else {
+        hipLaunchKernelGGL(lb_step_kernel<false>, dim3((unsigned)n_live), dim3(64), 0, st,
+                           A.states, A.part_sse, A.n_tiles, A.mode, A.part_mode, 0, 0, 0, 0, A);
+    }
     HIP_TRY(hipGetLastError());
     return DH_OK;
 }
