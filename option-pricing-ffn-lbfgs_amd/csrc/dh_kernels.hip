@@ -379,7 +379,8 @@ constexpr int kBatch = 64;
 // units when a request has few tables per slot) store T2_k in LDS and let the slot's first wave
 // re-form the same sums in the same order, so every slot width gives the same bits.
 template <int TPT>
-__global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(PriceArgs A) {
+__global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(PriceArgs A_) {
+    const PriceArgs& A = karg_ref<PriceArgs, 0>();   // read in place (karg_ref)
     if (halted(A)) return;
     constexpr int kTabs = kBlock / TPT;      // table slots per block
     extern __shared__ __attribute__((aligned(16))) double t2s[];   // TPT > 64: [kTabs][N] T2_k
@@ -915,7 +916,8 @@ constexpr int kRedDoubles = kR * kBlock;
 // option kernel
 // ----------------------------------------------------------------------------------------------
 template <int TPT, int RT>
-__global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(PriceArgs A) {
+__global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(PriceArgs A_) {
+    const PriceArgs& A = karg_ref<PriceArgs, 0>();   // read in place (karg_ref)
     if (halted(A)) return;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int kTasks = kBlock / TPT;
@@ -1045,7 +1047,8 @@ constexpr int small_rs(int max_nopt) { return max_nopt > 4 ? 8 : 4; }
 constexpr int64_t kSmallMinTasks = 65536;
 
 template <int RS>
-__global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A, int L) {
+__global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A_, int L) {
+    const PriceArgs& A = karg_ref<PriceArgs, 0>();   // read in place (karg_ref)
     if (halted(A)) return;
     const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t n_tasks = A.paired ? A.np : A.np * (int64_t)A.n_tiles;
