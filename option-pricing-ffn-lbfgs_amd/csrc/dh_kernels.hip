@@ -188,6 +188,30 @@ __device__ __forceinline__ double clamped_term_sum(const Params& P, double T, do
     return acc;
 }
 
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, Ctrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), Ctrl, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// s summed over its aligned group of `width` lanes (a power of two <= 64) exactly as the xor
+// butterfly s += __shfl_xor(s, off), off = 1, 2, 4, ... < width, sums it.  Levels 1 and 2 are DPP
+// quad permutes and levels 4 and 8 DPP half-row / row mirrors (a few cycles against a ds_bpermute
+// round trip each): after the lower levels every lane of a quad (half-row) holds the same value,
+// so the mirror partner's operand is the xor partner's and every sum is the same bits.  Levels
+// 16 and 32 stay ds_bpermute.  Every lane of the wave must be active.
+__device__ __forceinline__ double xor_sum(double s, int width) {
+    if (width > 1) s += dpp_f64<kDppXor1>(s);
+    if (width > 2) s += dpp_f64<kDppXor2>(s);
+    if (width > 4) s += dpp_f64<kDppHalfMirror>(s);
+    if (width > 8) s += dpp_f64<kDppMirror>(s);
+    for (int off = 16; off < width; off <<= 1) s += __shfl_xor(s, off, 64);
+    return s;
+}
+
 // per-table values staged in LDS by the prologue lane of the table:
 //   [0..5] a, b, e^b, e^a, 2/(b-a), pi/(b-a) | [6..21] CfConsts | [22] S0, [23] r, [24] T,
 //   [25] K/S0 below which the clamp test must be evaluated, [26] above which (prefilter),
@@ -461,10 +485,8 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             if (has && wv == 0) {
                 // c1 is a sum of zeros and w0 has one nonzero term (lane 0's): their butterflies
                 // would change no bit
-                for (int off = 1; off < 64; off <<= 1) {
-                    c0 += __shfl_xor(c0, off, 64);
-                    c5 += __shfl_xor(c5, off, 64);
-                }
+                c0 = xor_sum(c0, 64);
+                c5 = xor_sum(c5, 64);
                 if (lane == 0) {
                     red[i][0] = c0;
                     red[i][1] = c1;
@@ -508,7 +530,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                     const double bc = (x + 0.1 > b) ? x + 0.1 : b;
                     double v = clamped_term_sum(P, T, Kl, x, ac, bc, A.call[m] != 0, lane, 64, N,
                                                 sct);
-                    for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+                    v = xor_sum(v, 64);
                     if (lane == 0) A.cl_price[slot0 + base + l] = disc * v;
                 }
             }
@@ -719,7 +741,9 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     // lanes >= nopt hold +0.0 and only lane 0's sum is used, so levels with off >= nopt would add
     // +0.0 to it (an exact no-op on a sum of squares): skip them (C2's 32 options: 5 levels)
     const int lvl = nopt < 64 ? nopt : 64;
-    for (int off = 1; off < lvl; off <<= 1) s += __shfl_xor(s, off, 64);
+    int width = 1;
+    while (width < lvl) width <<= 1;
+    s = xor_sum(s, width);
     const double f = nb;
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
@@ -745,10 +769,8 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
         acc += __hip_atomic_load(&A.part_sse[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bad += __hip_atomic_load(&A.part_bad[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    for (int off = 1; off < 64; off <<= 1) {
-        acc += __shfl_xor(acc, off, 64);
-        bad += __shfl_xor(bad, off, 64);
-    }
+    acc = xor_sum(acc, 64);
+    bad = xor_sum(bad, 64);
     if (t == 0) {
         A.sse[p] = acc;
         A.n_bad[p] = (int)bad;
@@ -876,10 +898,8 @@ __device__ __forceinline__ void tile_sums_r(const PriceArgs& A, int64_t p, const
             __syncthreads();
             continue;
         }
-        for (int off = 1; off < G; off <<= 1) {
 #pragma unroll
-            for (int j = 0; j < RT; ++j) sm[j] += __shfl_xor(sm[j], off, 64);
-        }
+        for (int j = 0; j < RT; ++j) sm[j] = xor_sum(sm[j], G);
         if (pass == 0) DH_STAMP(A, 11);
         // every lane of the group holds the (bitwise identical) sums: lane j finalises option j
         if (G >= R) {
@@ -1198,10 +1218,8 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A_, 
         }
     }
     if (!A.part_sse) return;
-    for (int off = 1; off < L; off <<= 1) {
-        lsum += __shfl_xor(lsum, off, 64);
-        lbad += __shfl_xor(lbad, off, 64);
-    }
+    lsum = xor_sum(lsum, L);
+    lbad = xor_sum(lbad, L);
     if (!active || sub != 0) return;
     // fence-free hand-off (as task_loss): sc1 stores, drain, agent-scope ticket
     __hip_atomic_store(&A.part_sse[task], lsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1364,7 +1382,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
             const double bc = (x + 0.1 > b) ? x + 0.1 : b;
             double v = clamped_term_sum(P, T, L.K[base + l], x, ac, bc, L.call[base + l] != 0,
                                         lane, 64, N, sct);
-            for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+            v = xor_sum(v, 64);
             if (lane == 0) lclp[base + l] = disc * v;
         }
     }
@@ -1386,10 +1404,8 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
             c0 += T2 * eb * cb;
             c5 += T2 * ea;
         }
-        for (int off = 1; off < 64; off <<= 1) {
-            c0 += __shfl_xor(c0, off, 64);
-            c5 += __shfl_xor(c5, off, 64);
-        }
+        c0 = xor_sum(c0, 64);
+        c5 = xor_sum(c5, 64);
         if (lane == 0) {
             red[0][0] = c0;
             red[1][0] = 0.0;
@@ -1467,7 +1483,7 @@ __global__ __launch_bounds__(kBlock) void cos_exact_kernel(PriceArgs A, double* 
     const double a = (xK - 0.1 < a0) ? xK - 0.1 : a0;   // Python min/max semantics (:136-137)
     const double b = (xK + 0.1 > b0) ? xK + 0.1 : b0;
     double acc = exact_term_sum(P, T, K, xK, a, b, is_call, lane, 64, A.N);
-    for (int off = 1; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
+    acc = xor_sum(acc, 64);
     if (lane == 0) {
         const double price = exp(-P.r * T) * acc;
         if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
@@ -1489,10 +1505,8 @@ __global__ void loss_from_prices_kernel(const double* __restrict__ prices,
         acc += rel * rel;
         bad += (isnan(pr) || isinf(pr) || pr <= 0.0) ? 1.0 : 0.0;
     }
-    for (int off = 1; off < 64; off <<= 1) {
-        acc += __shfl_xor(acc, off, 64);
-        bad += __shfl_xor(bad, off, 64);
-    }
+    acc = xor_sum(acc, 64);
+    bad = xor_sum(bad, 64);
     if (lane == 0) {
         sse[s] = acc;
         n_bad[s] = (int)bad;
@@ -2561,14 +2575,6 @@ __device__ __forceinline__ WaveVec operator-(WaveVec a, WaveVec b) { return {a.v
 __device__ __forceinline__ WaveVec operator-(WaveVec a) { return {-a.v}; }
 __device__ __forceinline__ WaveVec operator*(double s, WaveVec a) { return {s * a.v}; }
 
-template <int Ctrl>
-__device__ __forceinline__ double dpp_f64(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, Ctrl, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), Ctrl, 0xf, 0xf, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
 
 __device__ __forceinline__ double row_sum(double p) {
     p = p + dpp_f64<kDppXor1>(p);
