@@ -197,18 +197,43 @@ __device__ __forceinline__ double dpp_f64(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// the value of lane ^ 16 (or lane ^ 32): v_permlane16_swap / v_permlane32_swap of v with itself
+// swap the odd rows (upper half) of the first copy with the even rows (lower half) of the second,
+// so the second copy holds the partner's value in the even rows (lower half) and the first in the
+// odd rows (upper half)
+template <bool k32>
+__device__ __forceinline__ double xor_partner(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    const bool upper = (__lane_id() & (k32 ? 32 : 16)) != 0;
+    unsigned plo, phi;
+    if constexpr (k32) {
+        const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        plo = upper ? l[0] : l[1];
+        phi = upper ? h[0] : h[1];
+    } else {
+        const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        plo = upper ? l[0] : l[1];
+        phi = upper ? h[0] : h[1];
+    }
+    return __longlong_as_double(((long long)phi << 32) | plo);
+}
+
 // s summed over its aligned group of `width` lanes (a power of two <= 64) exactly as the xor
-// butterfly s += __shfl_xor(s, off), off = 1, 2, 4, ... < width, sums it.  Levels 1 and 2 are DPP
-// quad permutes and levels 4 and 8 DPP half-row / row mirrors (a few cycles against a ds_bpermute
-// round trip each): after the lower levels every lane of a quad (half-row) holds the same value,
-// so the mirror partner's operand is the xor partner's and every sum is the same bits.  Levels
-// 16 and 32 stay ds_bpermute.  Every lane of the wave must be active.
+// butterfly s += __shfl_xor(s, off), off = 1, 2, 4, ... < width, sums it, without an LDS round
+// trip per level: levels 1 and 2 are DPP quad permutes, levels 4 and 8 DPP half-row / row mirrors
+// (after the lower levels every lane of a quad (half-row) holds the same value, so the mirror
+// partner's operand is the xor partner's and every sum is the same bits), levels 16 and 32
+// v_permlane16/32_swap.  Every lane of the wave must be active.
 __device__ __forceinline__ double xor_sum(double s, int width) {
     if (width > 1) s += dpp_f64<kDppXor1>(s);
     if (width > 2) s += dpp_f64<kDppXor2>(s);
     if (width > 4) s += dpp_f64<kDppHalfMirror>(s);
     if (width > 8) s += dpp_f64<kDppMirror>(s);
-    for (int off = 16; off < width; off <<= 1) s += __shfl_xor(s, off, 64);
+    if (width > 16) s += xor_partner<false>(s);
+    if (width > 32) s += xor_partner<true>(s);
     return s;
 }
 
