@@ -316,8 +316,19 @@ __device__ __forceinline__ const T& karg_ref() {
     const KargPtr k = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
     return *(const T*)(const char*)(k + off);
 }
-// FusedHead's arguments: 5 pointers and 2 ints, so PriceArgs starts at byte 48
+// FusedHead's arguments: 5 pointers and 2 ints, so PriceArgs starts at byte 48 (kernel arguments
+// are laid out in declaration order at their natural alignment, as the members of this struct)
 constexpr int kFusedArgsKernargOff = 48;
+struct FusedKargs {         // cos_fused_kernel's argument list as a struct (its kernarg layout)
+    const double* prm;
+    const double* tsrc;
+    const int2* groups;
+    const int* live;
+    const double* pre;
+    int tpp, paired;
+    PriceArgs A;
+};
+static_assert(offsetof(FusedKargs, A) == kFusedArgsKernargOff, "PriceArgs kernarg offset");
 
 // the live count read by launches without one (FusedHead::live): the halt test is then a load
 // like any other, with no branch on the pointer (a branch made the compiler wait for it at the
@@ -786,7 +797,7 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
         DH_STAMP(A, 15);
         old = __hip_atomic_fetch_add(&A.counter[p * kCounterStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    old = __shfl(old, 0, 64);
+    old = __builtin_amdgcn_readlane(old, 0);       // lane 0's ticket (no LDS round trip)
     DH_STAMP(A, 12);
     if (old != (unsigned)A.n_tiles - 1u) return;
     double acc = 0.0, bad = 0.0;
@@ -2721,6 +2732,13 @@ constexpr int kLbPre = 4;
 // byte offset of LbArgs in the kernel-argument segment: the leading arguments in declaration order
 // at their natural alignment (2 pointers, 3 + kLbPre ints = 44 bytes), then LbArgs 8-aligned
 constexpr int kLbArgsKernargOff = 48;
+struct LbKargs {            // lb_step_kernel's argument list as a struct (its kernarg layout)
+    void* states;
+    const double* part;
+    int ntiles, mode, part_mode, l[kLbPre];
+    LbArgs A;
+};
+static_assert(offsetof(LbKargs, A) == kLbArgsKernargOff, "LbArgs kernarg offset");
 
 // live_inline[slot] as a scalar load straight from the kernel-argument segment; indexing the
 // by-value argument compiled to a flat load
