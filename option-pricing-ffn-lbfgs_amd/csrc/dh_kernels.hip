@@ -1355,6 +1355,53 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
 
     const double a = shc[0], b = shc[1], eb = shc[2], ea = shc[3], scale = shc[4], piba = shc[5];
     const double T = shc[24];
+    // ---- clamp-widened options (double_heston.py:135-137), decided and priced per wave: the
+    //      masks first (a short loop), the pricing loop only where a mask is set (rare: its
+    //      register traffic stays off the common path).  The masks and prices are read after the
+    //      CF barrier, so the scan may run before or after the CF loop with the same bits: before
+    //      it in the 4-wave build (after it, the scan's LDS reads queue behind the table's stores
+    //      on the request's critical path: C2 -1.7%), after it in the 5-wave build (before it,
+    //      the register allocation of the <= 96-VGPR build costs C4 3%) ----
+    auto clamp_scan = [&]() {
+        bool any_cl = false;
+        for (int base = wv * 64; base < gn; base += nthr) {
+            const int o = base + lane;
+            bool cl = false;
+            if (o < gn) {
+                const double xK = L.xK[o];
+                cl = xK - 0.1 < a || xK + 0.1 > b;
+            }
+            const unsigned long long mask = __ballot(cl);
+            if (lane == 0) cmask[base / 64] = mask;
+            any_cl = any_cl || mask != 0;
+        }
+        if (__builtin_expect(any_cl, 0))
+        for (int base = wv * 64; base < gn; base += nthr) {
+            const int o = base + lane;
+            bool cl = false;
+            if (o < gn) {
+                const double xK = L.xK[o];
+                cl = xK - 0.1 < a || xK + 0.1 > b;
+            }
+            unsigned long long mask = __ballot(cl);
+            if (mask == 0) continue;
+            const Params P = dh::load_params(prm);
+            const double disc = exp(-P.r * T);
+            while (mask) {
+                const int l = __ffsll((long long)mask) - 1;
+                mask &= mask - 1;
+                const double x = L.xK[base + l];
+                const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
+                const double bc = (x + 0.1 > b) ? x + 0.1 : b;
+                double v = clamped_term_sum(P, T, L.K[base + l], x, ac, bc, L.call[base + l] != 0,
+                                            lane, 64, N, sct);
+                v = xor_sum(v, 64);
+                if (lane == 0) lclp[base + l] = disc * v;
+            }
+        }
+    };
+    constexpr bool kEarlyClamp = WV <= DH_FUSED_WAVES;
+    if constexpr (kEarlyClamp) clamp_scan();
     // ---- CF loop (threads < TPT1, one entry each up to N = 256): expanded table into LDS.
     //      (A lane pair per entry, one Heston factor each, cut C1 by 5% but cost C2 2%: the CF
     //      phase of a C2 request is issue-bound on the CUs that host two blocks.) ----
@@ -1383,45 +1430,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP_T(A, 17, 128);
         DH_STAMP_T(A, 18, 192);
     }
-    // ---- clamp-widened options (double_heston.py:135-137), decided and priced per wave: the
-    //      masks first (a short loop), the pricing loop only where a mask is set (rare: its
-    //      register traffic stays off the common path) ----
-    bool any_cl = false;
-    for (int base = wv * 64; base < gn; base += nthr) {
-        const int o = base + lane;
-        bool cl = false;
-        if (o < gn) {
-            const double xK = L.xK[o];
-            cl = xK - 0.1 < a || xK + 0.1 > b;
-        }
-        const unsigned long long mask = __ballot(cl);
-        if (lane == 0) cmask[base / 64] = mask;
-        any_cl = any_cl || mask != 0;
-    }
-    if (__builtin_expect(any_cl, 0))
-    for (int base = wv * 64; base < gn; base += nthr) {
-        const int o = base + lane;
-        bool cl = false;
-        if (o < gn) {
-            const double xK = L.xK[o];
-            cl = xK - 0.1 < a || xK + 0.1 > b;
-        }
-        unsigned long long mask = __ballot(cl);
-        if (mask == 0) continue;
-        const Params P = dh::load_params(prm);
-        const double disc = exp(-P.r * T);
-        while (mask) {
-            const int l = __ffsll((long long)mask) - 1;
-            mask &= mask - 1;
-            const double x = L.xK[base + l];
-            const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
-            const double bc = (x + 0.1 > b) ? x + 0.1 : b;
-            double v = clamped_term_sum(P, T, L.K[base + l], x, ac, bc, L.call[base + l] != 0,
-                                        lane, 64, N, sct);
-            v = xor_sum(v, 64);
-            if (lane == 0) lclp[base + l] = disc * v;
-        }
-    }
+    if constexpr (!kEarlyClamp) clamp_scan();
     DH_STAMP(A, 21);
     DH_STAMP_T(A, 22, 64);
     __syncthreads();
