@@ -376,17 +376,20 @@ class Surface:
         return sse, bad, prices
 
     def calibrate_lbfgs(self, x0s, S0, r, N=128, L=10.0, *, maxiter=300, maxfun=15000, maxls=20,
-                        ftol=1e-9, gtol=1e-6, chunk=8):
+                        ftol=1e-9, gtol=1e-6, chunk=8, ctx=None):
         """Device-resident L-BFGS-B for every row of x0s [S, 13] (dh_calibrate_lbfgs).
+        ctx: the context (stream and scratch) to run on, default the surface's; a surface may be
+        used by several contexts of its device at once.
         -> (list of LbResult, number of loss launches)."""
+        ctx = ctx or self.ctx
         x0s = _f64(x0s).reshape(-1, 13)
         S = x0s.shape[0]
         opt = LbOptions(int(maxiter), int(maxfun), int(maxls), int(chunk), float(ftol),
                         float(gtol))
         res = (LbResult * max(S, 1))()
         nl = C.c_int32(0)
-        with self.ctx._lock:
-            _check(load().dh_calibrate_lbfgs(self.ctx.handle, self._h, _ptr(x0s), S, float(S0),
+        with ctx._lock:
+            _check(load().dh_calibrate_lbfgs(ctx.handle, self._h, _ptr(x0s), S, float(S0),
                                              float(r), int(N), float(L), C.byref(opt), res,
                                              C.byref(nl)))
         return list(res)[:S], nl.value
