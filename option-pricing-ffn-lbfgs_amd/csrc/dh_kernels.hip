@@ -240,8 +240,8 @@ __device__ __forceinline__ double xor_sum(double s, int width) {
 // per-table values staged in LDS by the prologue lane of the table:
 //   [0..5] a, b, e^b, e^a, 2/(b-a), pi/(b-a) | [6..21] CfConsts | [22] S0, [23] r, [24] T,
 //   [25] K/S0 below which the clamp test must be evaluated, [26] above which (prefilter),
-//   [27] group's first option, [28] group size (as doubles)
-constexpr int kTabC = 29;
+//   [27] group's first option, [28] group size (as doubles), [29] the discount e^{-rT}
+constexpr int kTabC = 30;
 constexpr double kClampMargin = 1e-9;   // relative safety margin of the K-space prefilter
 static_assert(sizeof(dh::CfConsts) == 16 * sizeof(double), "CfConsts layout");
 
@@ -276,6 +276,7 @@ __device__ __forceinline__ void table_prologue(const PriceArgs& A, int64_t q, do
     c[26] = exp(b - 0.1) * (1.0 - kClampMargin);
     c[27] = gr.x;
     c[28] = gr.y;
+    c[29] = exp(-P.r * T);
 }
 
 // table_prologue run by one wave in lockstep (the fused kernel's wave 0): the two variance
@@ -355,9 +356,10 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const Fu
                       P.lam * T * (P.sj * P.sj + P.muj * P.muj);
     const double h = A.L * sqrt(fabs(c2));
     const double a = c1 - h, b = c1 + h;           // trunc_unclamped (double_heston.py:120-132)
-    const int e_lane = lane < 5 ? lane : 0;
+    const int e_lane = lane < 6 ? lane : 0;
     const double arg = e_lane == 0 ? b : e_lane == 1 ? a : e_lane == 2 ? a + 0.1
-                     : e_lane == 3 ? b - 0.1 : P.muj + 0.5 * (P.sj * P.sj);
+                     : e_lane == 3 ? b - 0.1 : e_lane == 4 ? P.muj + 0.5 * (P.sj * P.sj)
+                     : -P.r * T;
     const double e = exp(arg);
     dh::CfConsts CC;
     double* f1 = (double*)&CC.f1;
@@ -388,6 +390,7 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const Fu
         c[26] = lane_bcast(e, 3) * (1.0 - kClampMargin);
         c[27] = gr.x;
         c[28] = gr.y;
+        c[29] = lane_bcast(e, 5);
     }
 }
 
@@ -1440,25 +1443,32 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     //      bits as cos_table_kernel).  c1 is a sum of zeros (+0.0) and w0 has one nonzero term
     //      (lane 0's), so their butterflies change no bit and are skipped || per-option
     //      rotations ----
-    if (wv == 0) {
+    // c0 on wave 0 and c5 on the block's last wave (wave 1 stages the rotations): each wave runs
+    // one sum's chain, in the same lane order and butterfly, so the same bits (4-wave build; the
+    // 5-wave build keeps both on wave 0: its register allocation cost C4 2%)
+    const int w5 = (WV <= DH_FUSED_WAVES && nthr >= 192) ? nthr / 64 - 1 : 0;
+    if (wv == 0 || wv == w5) {
+        const bool f0 = wv == 0, f5 = wv == w5;
         double c0 = 0.0, c5 = 0.0;
         for (int k = lane; k < N; k += 64) {
             if (k == 0) continue;
             const double T2 = L.t26[k].x;
             const double cb = (k & 1) ? -1.0 : 1.0;
-            c0 += T2 * eb * cb;
-            c5 += T2 * ea;
+            if (f0) c0 += T2 * eb * cb;
+            if (f5) c5 += T2 * ea;
         }
-        c0 = xor_sum(c0, 64);
-        c5 = xor_sum(c5, 64);
+        if (f0) c0 = xor_sum(c0, 64);
+        if (f5) c5 = xor_sum(c5, 64);
         if (lane == 0) {
-            red[0][0] = c0;
-            red[1][0] = 0.0;
-            red[2][0] = c5;
-            red[3][0] = w0s;
+            if (f0) {
+                red[0][0] = c0;
+                red[1][0] = 0.0;
+                red[3][0] = w0s;
+            }
+            if (f5) red[2][0] = c5;
         }
     }
-    const double disc = exp(-shc[23] * T);          // r staged by the prologue: no global load
+    const double disc = shc[29];                    // e^{-rT}, staged by the prologue
     const int G = group_lanes<RT>(gn, N, tpt2);
     {
         const double ustep = G * dh::kPi / (b - a);
