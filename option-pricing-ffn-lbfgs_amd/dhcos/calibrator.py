@@ -115,8 +115,9 @@ def fd_models(X0, h=FD_ABS_STEP):
     fg_from_losses() bit for bit)."""
     X0 = np.asarray(X0, dtype=np.float64)
     Xh = X0 + h
-    vanish = (Xh - X0) == 0
-    if vanish.any():
+    d = Xh - X0
+    if np.count_nonzero(d) != d.size:                 # some step vanishes (d == 0); NaN counts
+        vanish = d == 0                                # as nonzero, as in (Xh - X0) == 0
         sign = np.where(X0 >= 0, 1.0, -1.0)
         Xh = X0 + np.where(vanish, _SQRT_EPS * sign * np.maximum(1.0, np.abs(X0)), h)
     XX = np.concatenate([X0, Xh])
@@ -401,7 +402,8 @@ def lbfgsb_steps(x0, maxiter, maxfun, m=10, ftol=1e-9, gtol=1e-6, maxls=20):
         _lbfgsb.setulb(m, x, low_bnd, upper_bnd, nbd, f, g, factr, pgtol, wa, iwa, task, lsave,
                        isave, dsave, maxls, ln_task)
         if task[0] == 3:
-            if not np.array_equal(x, sf_x):          # ScalarFunction.fun_and_grad
+            if not (x == sf_x).all():                # ScalarFunction.fun_and_grad: np.array_equal
+                                                     # (same shapes, so its elementwise test)
                 sf_x = x.astype(np.float64)
                 sf_f, sf_g = yield sf_x
                 nfev += 1
@@ -520,7 +522,7 @@ def _advance(cal, gens, states, order, outcomes):
         while pending:
             ids = sorted(pending)
             try:
-                X0 = np.stack([pending[sid] for sid in ids])
+                X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
                 f0, G, lows = (cal.fg_batch(X0) if hasattr(cal, "fg_batch")
                                else fg_from_losses(cal, X0))
             except _native.NativeError:
@@ -580,7 +582,7 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
         inflight[k] = None
         if not ids:
             return
-        X0 = np.stack([pending[sid] for sid in ids])
+        X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
         try:
             model = fd_models(X0)
         except Exception:          # reference: except -> continue (the starts are dropped)
