@@ -104,3 +104,29 @@ def test_warm_start_hook_replaces_start_zero_only(calib_golden):
     np.random.seed(3)
     vec = cal.start_points(4, x0=plain[2])
     assert np.array_equal(vec[0], plain[2]) and np.array_equal(vec[3], plain[3])
+
+
+def test_fd_models_equals_per_point_transforms():
+    """fd_models (the SciPy driver's per-request transforms, three ufunc calls over the request)
+    equals x_to_model of every FD point fd_request_points_many forms, bit for bit: at ordinary
+    points, where the absolute step vanishes (|x| ~ 1e9: the relative step), at +-0, and with a
+    NaN component (no step vanishes there: NaN - NaN compares unequal to 0)."""
+    from dhcos.calibrator import fd_models, fd_request_points_many, x_to_model
+    rs = np.random.RandomState(7)
+    for case in range(40):
+        S = 1 + case % 3
+        X0 = rs.normal(0.0, 1.5, size=(S, N_PARAMS))
+        if case % 4 == 1:
+            X0[rs.randint(S), rs.randint(N_PARAMS)] = rs.choice([1e9, -3e9, 7.5e8])
+        if case % 4 == 2:
+            X0[rs.randint(S), rs.randint(N_PARAMS)] = rs.choice([0.0, -0.0])
+        if case % 4 == 3:
+            X0[rs.randint(S), rs.randint(N_PARAMS)] = np.nan
+        P = fd_models(X0)
+        X, _ = fd_request_points_many(X0)
+        want = x_to_model(X).reshape(S, N_PARAMS + 1, N_PARAMS)
+        with np.errstate(invalid="ignore"):
+            assert np.array_equal(P[0].view(np.int64), want[:, 0].view(np.int64)), case
+            for i in range(N_PARAMS):        # point i + 1 moves component i only
+                assert np.array_equal(P[1][:, i].view(np.int64),
+                                      want[:, i + 1, i].view(np.int64)), (case, i)
