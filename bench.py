@@ -1,22 +1,27 @@
 #!/usr/bin/env python3
 """Benchmark: option-prices/sec (+ calibrations/sec) of the COS calibration objective on MI355X.
 
-Workload (BASELINE.json configs[1], the single-GPU config the metric is quoted on):
-  "c2": a 1,024-option synthetic surface (32 K/S in linspace(0.8, 1.2) x 32 T in
-  linspace(0.1, 2.0), calls, S0 = 100, r = 0.03, market = model at a seed-1 parameter draw x
-  (1 + N(0, 0.02)), seed 2), COS N = 256.  One step = one L-BFGS-B function+gradient request =
-  the 14 SciPy forward-difference points (13 parameters + base) priced over all 1,024 options and
-  reduced to 14 losses: 14,336 option prices per step.  Each step uses a different x (different
-  param sets), all inputs resident in HBM before the timed region; the steps are issued back to
-  back on one stream (independent requests, as in lockstep multi-start).
+Default workload "c3" (BASELINE.json configs[2]): the metric is quoted at COS N = 128, which no
+single-GPU config runs, so the line is the largest single-GPU configuration -- the north star's
+10k-option calibration: a 10,000-option synthetic surface (100 K/S in linspace(0.8, 1.2) x 100 T
+in linspace(0.1, 2.0), puts below the spot and calls at or above it, S0 = 100, r = 0.03, market =
+model at a seed-1 parameter draw x (1 + N(0, 0.02)), seed 2), COS N = 512, 3 lockstep L-BFGS-B
+starts.  One step = one lockstep function+gradient request = 3 starts x the 14 SciPy forward-
+difference points (13 parameters + base) priced over all 10,000 options and reduced to 42 losses:
+420,000 option prices per step.  Each step uses a different x (different param sets), all inputs
+resident in HBM before the timed region; the steps are issued back to back on one stream.
+Also: --config c2 (configs[1]: 1,024 options, N = 256, one start), c1, c4 (64 starts), c5 (the
+generator batch, 1M x 32 options).
 
 Multi-GPU (torchrun, one process per GPU): weak scaling -- every rank runs its own independent
 requests (multi-start sharding has no data-path collective); timing is the max over ranks;
 value = all ranks' prices / that time.
 
-Also reported: roofline of the dominant kernel (cos_price_kernel) from HIP events on its stream,
-a full single-start calibration of the same surface (calibrations/sec), and a CPU baseline (the
-scalar-structured NumPy port in oracle/, timed on a bounded sample on rank 0).
+Also reported: the roofline of the request kernel (HIP events on its stream; frac = the fp64
+flops the hardware executed per request, from the committed rocprofv3 counter pass, over this
+run's request time), full calibrations of the same surface (calibrations/sec, both optimizer
+drivers) and a CPU baseline (the scalar-structured NumPy port in oracle/, timed on a bounded
+sample on rank 0, anchored to the reference by profiles/cpu_anchor.json).
 """
 import argparse
 import json
@@ -104,6 +109,34 @@ def _cpu_worker(args):
     return n, time.perf_counter() - t0
 
 
+def cpu_model():
+    """This host's CPU model (the cpu_baseline's cores)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def reference_anchor(N):
+    """The reference's pricing(N) time over the port's, measured side by side in the build
+    container (tools/cpu_anchor.py -> profiles/cpu_anchor.json; the reference never travels to the
+    GPU box), at the nearest N measured."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_anchor.json")) as fh:
+            a = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    row = min(a["rows"], key=lambda r: abs(r["N"] - N))
+    return {"reference_over_port_time": row["reference_over_port_time"], "at_N": row["N"],
+            "reference_ms_per_option": row["reference_ms_per_option"],
+            "port_ms_per_option": row["port_ms_per_option"],
+            "measured_on": a["cpu_model"], "source": "profiles/cpu_anchor.json"}
+
+
 def cpu_baseline(cal_opts, S0, r, N, budget_s=12.0, cores=None):
     """Scalar-structured NumPy port (oracle/) of the reference pricer on `cores` host processes
     (default: 16, the GPU box's CPU share), each on a bounded sample of the
@@ -122,11 +155,16 @@ def cpu_baseline(cal_opts, S0, r, N, budget_s=12.0, cores=None):
     n = sum(c for c, _ in res)
     rate = sum(c / t for c, t in res)
     wall = max(t for _, t in res)
-    return {"value": rate, "unit": "option-prices/s", "cores": cores, "kind": "port",
-            "per_core": rate / cores,
-            "sample": f"{n} options of the workload priced one by one at N={N} by "
-                      f"oracle.dh_oracle.price_scalar (reference algorithm restated) in "
-                      f"{cores} processes x {wall:.1f} s"}
+    out = {"value": rate, "unit": "option-prices/s", "cores": cores, "kind": "port",
+           "cpu_model": cpu_model(), "per_core": rate / cores,
+           "sample": f"{n} options of the workload priced one by one at N={N} by "
+                     f"oracle.dh_oracle.price_scalar (reference algorithm restated) in "
+                     f"{cores} processes x {wall:.1f} s"}
+    anchor = reference_anchor(N)
+    if anchor:
+        out["reference_anchor"] = anchor
+        out["reference_equivalent_value"] = rate / anchor["reference_over_port_time"]
+    return out
 
 
 def cpu_options(cfg):
@@ -166,9 +204,9 @@ def pmc_traffic(config):
 
 
 def pmc_executed(config, ker_ms, launches=1):
-    """Executed fp64 flops of one request (rocprofv3 SQ_INSTS_VALU_*_F64 of its kernels, committed
-    under profiles/) over this run's request time: the hardware rate, beside the convention-based
-    `achieved` (whose per-entry / per-term counts are frozen)."""
+    """Executed fp64 flops of one request (rocprofv3 SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64
+    lanes of its kernels, FMA = 2, committed under profiles/) over this run's request time: the
+    rate the hardware sustained, independent of any counting convention."""
     ks = _pmc(config).get("kernels", {})
     fl = [k.get("exec_fp64_flop") for k in ks.values()]
     if not fl or any(f is None for f in fl):
@@ -176,6 +214,42 @@ def pmc_executed(config, ker_ms, launches=1):
     tf = sum(fl) * launches / (ker_ms * 1e-3) / 1e12
     return {"exec_fp64_flop_per_request": sum(fl) * launches, "TFLOPs": round(tf, 3),
             "frac": round(tf / PEAK_FP64_TFLOPS, 4), "source": f"profiles/pmc_traffic.json [{config}]"}
+
+
+def make_roofline(flop_conv, survey_flop, ker_ms, executed, traffic, alg_bytes, label,
+                  **extra):
+    """The roofline object: `frac` is the counter-executed fp64 fraction of the request (the only
+    hardware-anchored figure: the frozen convention charges the round-1 kernels' flops, and
+    SURVEY 8(d)'s per-term trig is replaced here by table + recurrence, so it exceeds 1 on C3);
+    both conventions are reported beside it.  Without a committed counter pass for the config
+    the frozen convention stands in (flop_basis says which)."""
+    conv_tf = flop_conv / (ker_ms * 1e-3) / 1e12
+    if executed:
+        ach, basis = executed["TFLOPs"], ("executed fp64 flops per request (rocprofv3 "
+                                          "SQ_INSTS_VALU_*_F64 x 64 lanes, FMA = 2, "
+                                          + executed["source"] + ") / request time")
+        flop = executed["exec_fp64_flop_per_request"]
+    else:
+        ach, basis, flop = conv_tf, "frozen convention (no counter pass committed)", flop_conv
+    r = {"bound": "valu_fp64", "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS,
+         "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": traffic,
+         "flop_basis": basis, "flop_per_launch": flop, "kernel": label,
+         "kernel_ms": round(ker_ms, 5),
+         "convention": {"flop_per_launch": flop_conv, "achieved_TFLOPs": round(conv_tf, 3),
+                        "frac": round(conv_tf / PEAK_FP64_TFLOPS, 4),
+                        "counts": f"FLOP_TAB {FLOP_TAB} / FLOP_TERM {FLOP_TERM} / FLOP_OPT "
+                                  f"{FLOP_OPT} (bench.py, frozen in round 1)"},
+         "survey_8d": {"flop_eq_per_launch": survey_flop,
+                       "achieved_TFLOPs": round(survey_flop / (ker_ms * 1e-3) / 1e12, 3),
+                       "frac": round(survey_flop / (ker_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4),
+                       "note": "716 flop-eq per CF + 120 per (set, option, k): charges per-term "
+                               "trig the kernels replace by table + recurrence (DESIGN.md 4)"},
+         "alg_bytes_per_launch": alg_bytes,
+         "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
+                 "peak_GBs": PEAK_HBM_GBS,
+                 "frac": alg_bytes / (ker_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}}
+    r.update(extra)
+    return r
 
 
 CONFIGS = {
@@ -289,6 +363,7 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
     ker_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
     G = 4
     flop = P * G * N * FLOP_TAB + P * M * (N - 1) * FLOP_TERM + P * M * FLOP_OPT
+    survey_flop = P * G * N * 716 + P * M * N * 120
     alg_bytes = P * 16 * 8 + M * 17 + P * M * 8
     # launch pairs per batch: the library chunks param sets so one chunk's tables stay within
     # 256 MiB (dh_kernels.hip launch_price: per set = groups x (N + 8 consts + clamp words +
@@ -296,17 +371,11 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
     per_p = G * (N + 8 + 1 + 8) * 8
     n_chunks = -(-P // max(1, (256 << 20) // per_p))
     tr = pmc_traffic(args.config)
-    roofline = {"bound": "valu_fp64", "achieved": round(flop / (ker_ms * 1e-3) / 1e12, 3),
-                "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(flop / (ker_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4),
-                "traffic": tr * n_chunks if tr else None, "launch_pairs": n_chunks,
-                "kernel": kernel_label(surf.ctx) + " (all chunks of one batch, HIP events)",
-                "kernel_ms": round(ker_ms, 4), "flop_per_launch": flop,
-                "executed": pmc_executed(args.config, ker_ms, n_chunks),
-                "alg_bytes_per_launch": alg_bytes,
-                "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
-                        "peak_GBs": PEAK_HBM_GBS,
-                        "frac": alg_bytes / (ker_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}}
+    roofline = make_roofline(flop, survey_flop, ker_ms,
+                             pmc_executed(args.config, ker_ms, n_chunks),
+                             tr * n_chunks if tr else None, alg_bytes,
+                             kernel_label(surf.ctx) + " (all chunks of one batch, HIP events)",
+                             launch_pairs=n_chunks)
     if rank == 0:
         line = {"metric": "option-prices/sec (COS, generator batch)", "value": value,
                 "unit": "option-prices/s", "n_gpus": world, "steps": args.steps,
@@ -364,7 +433,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-calib", action="store_true", help="skip the full-calibration leg")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -480,21 +549,11 @@ def main():
     n_tiles = surf.n_tiles
     groups = len({o["maturity"] for o in opts})
     flop = S * groups * N * FLOP_TAB + S * M * (N - 1) * FLOP_TERM + S * M * FLOP_OPT
-    achieved = flop / (ker_ms * 1e-3) / 1e12
     alg_bytes = S * 16 * 8 + S * M * BYTES_PER_OPTION + S * n_tiles * 12 + S * 12
     survey_flop = S * groups * N * 716 + S * M * N * 120        # SURVEY 8(d) convention
-    roofline = {"bound": "valu_fp64", "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4),
-                "traffic": pmc_traffic(args.config),
-                "kernel": kernel_label(surf.ctx) + " (one request, HIP events)",
-                "kernel_ms": round(ker_ms, 5), "flop_per_launch": flop,
-                "executed": pmc_executed(args.config, ker_ms),
-                "alg_bytes_per_launch": alg_bytes,
-                "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
-                        "peak_GBs": PEAK_HBM_GBS,
-                        "frac": alg_bytes / (ker_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
-                "survey_convention": {"flop_eq_per_launch": survey_flop,
-                                      "achieved_TFLOPs": survey_flop / (ker_ms * 1e-3) / 1e12}}
+    roofline = make_roofline(flop, survey_flop, ker_ms, pmc_executed(args.config, ker_ms),
+                             pmc_traffic(args.config), alg_bytes,
+                             kernel_label(surf.ctx) + " (one request, HIP events)")
 
     # ---- calibrations/sec: one full calibration of the same surface; at N > 1 its starts are
     # sharded over the ranks (dhcos.distributed; 3 starts per GPU, weak scaling; c4: 64 starts

@@ -32,7 +32,10 @@ extern "C" {
 #endif
 
 #define DH_PARAM_STRIDE 16
-#define DH_MAX_N 2048            /* largest COS series length accepted (LDS-resident table) */
+#define DH_MAX_N 2048            /* longest COS series of the table (fast) path: LDS-resident */
+#define DH_MAX_N_PER_TERM 65536  /* longest accepted: N > DH_MAX_N runs the per-term path (the
+                                    reference's operation order, one wave per option), slower
+                                    but any length the reference's pricing(N) takes up to here  */
 
 enum {
     DH_OK = 0,
@@ -137,8 +140,13 @@ int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0, const doub
  * run in enqueue order; 14 S <= 1024 (larger: dh_surface_fg).                                   */
 int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const double* x0, const double* model,
                         int S, double S0, double r, int N, double L, int slot);
-int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, double* f, double* g,
+/* end: S must be the start count the slot's request was enqueued with, and s its surface
+ * (DH_E_ARG otherwise, the request stays in flight): f[S], g[S][13], low[S] are written.
+ * cancel: wait for the slot's request (if any) and discard it, so the slot is free again (a
+ * driver unwinding from an error); no-op on an idle slot.                                      */
+int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, int S, double* f, double* g,
                       double* low);
+int dh_surface_fg_cancel(dh_ctx* ctx, int slot);
 
 /* ---- device-resident multi-start L-BFGS-B ------------------------------------------------- */
 /* Runs S independent L-BFGS-B starts (no bounds) on the surface's calibration loss without a
@@ -225,6 +233,10 @@ int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const dou
 /* phi(u_j; tau) for one param set: DoubleHeston.characteristic_function (double_heston.py:48-97) */
 int dh_cf(dh_ctx* ctx, const double* params, const double* u, int n, double tau, double* re,
           double* im);
+/* The same at complex frequencies phi_j = u_re[j] + i u_im[j] (the reference documents
+ * phi : complex, double_heston.py:48-61, and evaluates it with complex arithmetic throughout)  */
+int dh_cf_complex(dh_ctx* ctx, const double* params, const double* u_re, const double* u_im,
+                  int n, double tau, double* re, double* im);
 /* [a_i, b_i] for param set i and option i: DoubleHeston.truncationRange (double_heston.py:100-139) */
 int dh_trunc_range(dh_ctx* ctx, const double* params, const double* K, const double* T,
                    int64_t P, double L, double* a, double* b);

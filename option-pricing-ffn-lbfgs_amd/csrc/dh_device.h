@@ -339,7 +339,9 @@ __device__ __forceinline__ double datan2_t(double y, double x, const double2* __
     const double ax = fabs(x), ay = fabs(y);
     const double mx = fmax(ax, ay), mn = fmin(ax, ay);
     const double t0 = mn * __builtin_amdgcn_rcp(mx);
-    const int j = (int)rint(t0 * 64.0);                              // 0 .. 64
+    // 0 .. 64; clamped in fp so a NaN t0 (NaN operands, or D conj(d) = 0) indexes entry 0
+    // instead of converting NaN to int (poison) -- a NaN there already makes the price NaN
+    const int j = (int)fmin(fmax(rint(t0 * 64.0), 0.0), 64.0);
     const double sj = (double)j * 0.015625;
     const double xp = fma(mn, sj, mx), yp = fma(-mx, sj, mn);
     const double tp = yp * drcp(xp);
@@ -406,6 +408,47 @@ __device__ __forceinline__ cplx cf_eval(const Params& P, double u, double tau) {
     const double lt = P.lam * tau;
     const cplx jump = cexp_({lt * (ej.re - 1.0), lt * ej.im});        // :93
     const cplx ex = {A.re + B1.re * P.v01 + B2.re * P.v02, A.im + B1.im * P.v01 + B2.im * P.v02};
+    return cmul(cexp_(ex), jump);                                     // :94-96
+}
+
+// One variance factor at a complex frequency phi (double_heston.py:64-71 / :73-80, :85-91), in
+// the reference's operation order on complex operands: beta = kappa - rho sigma i phi, d =
+// sqrt(beta^2 + sigma^2 phi (phi + i)), the same g, B and log terms as heston_factor.
+__device__ __forceinline__ cplx heston_factor_z(cplx phi, double tau, double kap, double th,
+                                                double sig, double rho, cplx& A) {
+    const cplx iphi = {-phi.im, phi.re};                  // i phi
+    const cplx beta = csub({kap, 0.0}, cscale(iphi, rho * sig));
+    const double s2 = sig * sig;
+    const cplx quad = cmul(cscale(phi, s2), {phi.re, phi.im + 1.0});   // sigma^2 phi (phi + i)
+    const cplx d = csqrt_p(cadd(cmul(beta, beta), quad));
+    const cplx bm = csub(beta, d);
+    const cplx g = cdiv(bm, cadd(beta, d));
+    const cplx e = cexp_({-(d.re * tau), -(d.im * tau)});
+    const cplx ge = cmul(g, e);
+    const cplx one_m_ge = {1.0 - ge.re, -ge.im};
+    const cplx B = cmul(cdiv(bm, {s2, 0.0}), cdiv({1.0 - e.re, -e.im}, one_m_ge));
+    const cplx lg = clog_(cdiv(one_m_ge, {1.0 - g.re, -g.im}));
+    const double coef = (kap * th) / s2;
+    const cplx inner = {bm.re * tau - 2.0 * lg.re, bm.im * tau - 2.0 * lg.im};
+    A = cadd(A, cscale(inner, coef));
+    return B;
+}
+
+// phi at a complex frequency (double_heston.py:48-97 documents phi : complex): the reference's
+// expressions with complex phi throughout, for DoubleHeston.characteristic_function on complex
+// input (dh_cf_complex).  Matches the reference to ~1e-14 relative, not bit for bit.
+__device__ __forceinline__ cplx cf_eval_z(const Params& P, cplx phi, double tau) {
+    const double comp = exp(P.muj + 0.5 * (P.sj * P.sj)) - 1.0;      // :82
+    const cplx iphi = {-phi.im, phi.re};
+    cplx A = cscale(iphi, (P.r - P.q - P.lam * comp) * tau);         // :83
+    const cplx B1 = heston_factor_z(phi, tau, P.k1, P.t1, P.s1, P.r1, A);
+    const cplx B2 = heston_factor_z(phi, tau, P.k2, P.t2, P.s2, P.r2, A);
+    const cplx phi2 = cmul(phi, phi);
+    const cplx arg = csub(cscale(iphi, P.muj), cscale(phi2, 0.5 * (P.sj * P.sj)));
+    const cplx ej = cexp_(arg);                                       // e^{i phi mu - sj^2 phi^2/2}
+    const double lt = P.lam * tau;
+    const cplx jump = cexp_({lt * (ej.re - 1.0), lt * ej.im});        // :93
+    const cplx ex = {A.re + (B1.re * P.v01) + (B2.re * P.v02), A.im + (B1.im * P.v01) + (B2.im * P.v02)};
     return cmul(cexp_(ex), jump);                                     // :94-96
 }
 

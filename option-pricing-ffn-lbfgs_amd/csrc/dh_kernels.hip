@@ -1581,6 +1581,17 @@ __global__ void cf_kernel(const double* __restrict__ prm, const double* __restri
     im[i] = c.im;
 }
 
+__global__ void cf_kernel_z(const double* __restrict__ prm, const double* __restrict__ ure,
+                            const double* __restrict__ uim, int n, double tau,
+                            double* __restrict__ re, double* __restrict__ im) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Params P = dh::load_params(prm);
+    const cplx c = dh::cf_eval_z(P, {ure[i], uim[i]}, tau);
+    re[i] = c.re;
+    im[i] = c.im;
+}
+
 __global__ void trunc_kernel(const double* __restrict__ prm, const double* __restrict__ K,
                              const double* __restrict__ T, int64_t P, double L,
                              double* __restrict__ a, double* __restrict__ b) {
@@ -1725,11 +1736,16 @@ struct dh_ctx {
     HostBuf h_lb;              // finished flags / live list of dh_calibrate_lbfgs
     // the two in-flight slots of dh_surface_fg_begin / _end: zero-copy records in, sse / n_bad
     // out, the host-side Feller terms and FD steps, and the request's completion event
-    size_t fg_max_units = 0;   // largest (param sets x tasks) of any dh_surface_fg_begin request
+    // largest (param sets x tasks) of any dh_surface_fg_begin request on (fg_surf, fg_N): the
+    // scratch reservations are a function of the surface, N and the param-set count only
+    size_t fg_max_units = 0;
+    const dh_surface* fg_surf = nullptr;
+    int fg_N = 0;
     struct FgSlot {
         HostBuf h_params, h_loss;
         std::vector<double> pen, dx;
         int S = 0, M = 0;
+        const dh_surface* surf = nullptr;   // the surface the request was enqueued on
         bool pending = false;
         hipEvent_t done = nullptr;
     } fg[2];
@@ -1767,6 +1783,10 @@ struct dh_surface {
 };
 
 namespace {
+
+// Requests run the per-term path (cos_exact_kernel) in validation mode, and for series longer
+// than the fast path's LDS-resident table holds (N > DH_MAX_N).
+bool per_term(const dh_ctx* ctx, int N) { return ctx->exact || N > DH_MAX_N; }
 
 // Busy-wait for a short request (a calibration iteration waits on it): polling hipStreamQuery
 // returns as soon as the stream drains, where hipStreamSynchronize may yield the thread.
@@ -1837,8 +1857,8 @@ int ensure_attrs(dh_ctx* ctx) {
 }
 
 int check_N(int N) {
-    if (N < 1 || N > DH_MAX_N)
-        return fail(DH_E_ARG, "N must be in [1, " + std::to_string(DH_MAX_N) + "], got " +
+    if (N < 1 || N > DH_MAX_N_PER_TERM)
+        return fail(DH_E_ARG, "N must be in [1, " + std::to_string(DH_MAX_N_PER_TERM) + "], got " +
                                   std::to_string(N));
     return DH_OK;
 }
@@ -2315,7 +2335,7 @@ int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_param
     DeviceScope dev_scope(ctx->device);
     if (dev_scope.rc) return dev_scope.rc;
     PriceArgs A = surface_args(s, d_params, P, N, L);
-    A.exact = ctx->exact;
+    A.exact = per_term(ctx, N);
     A.out = d_out;
     return launch_price(ctx, A, stream ? (hipStream_t)stream : ctx->stream);
 }
@@ -2350,7 +2370,7 @@ static int surface_loss_launch(dh_ctx* ctx, const dh_surface* s, const double* d
         HIP_TRY(hipMemsetAsync(ctx->counter.ptr, 0, ctx->counter.cap, st));
     }
     PriceArgs A = surface_args(s, d_params, S, N, L);
-    A.exact = ctx->exact;
+    A.exact = per_term(ctx, N);
     A.out = d_prices;
     A.part_sse = (double*)ctx->part_sse.ptr;
     A.part_bad = (int*)ctx->part_bad.ptr;
@@ -2505,7 +2525,7 @@ int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const dou
     A.opt_cap = 2;
     A.max_group = 1;
     A.M = (int)P;
-    A.exact = ctx->exact;
+    A.exact = per_term(ctx, N);
     A.strike_mode = DH_STRIKE_ABSOLUTE;
     A.N = N;
     A.L = L;
@@ -2545,6 +2565,35 @@ int dh_cf(dh_ctx* ctx, const double* params, const double* u, int n, double tau,
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(re, ctx->aux1.ptr, vb, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(im, ctx->aux2.ptr, vb, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return DH_OK;
+}
+
+int dh_cf_complex(dh_ctx* ctx, const double* params, const double* u_re, const double* u_im,
+                  int n, double tau, double* re, double* im) {
+    if (!ctx || !params || (n > 0 && (!u_re || !u_im || !re || !im)))
+        return fail(DH_E_ARG, "null argument");
+    if (n < 0) return fail(DH_E_ARG, "n < 0");
+    if (n == 0) return DH_OK;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
+    const size_t vb = (size_t)n * 8;
+    HIP_TRY(ctx->params.reserve(DH_PARAM_STRIDE * 8));
+    HIP_TRY(ctx->aux0.reserve(vb));
+    HIP_TRY(ctx->aux1.reserve(vb));
+    HIP_TRY(ctx->aux2.reserve(vb));
+    HIP_TRY(ctx->aux3.reserve(vb));
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(ctx->params.ptr, params, DH_PARAM_STRIDE * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->aux0.ptr, u_re, vb, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->aux1.ptr, u_im, vb, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(cf_kernel_z, dim3((n + 255) / 256), dim3(256), 0, st,
+                       (const double*)ctx->params.ptr, (const double*)ctx->aux0.ptr,
+                       (const double*)ctx->aux1.ptr, n, tau, (double*)ctx->aux2.ptr,
+                       (double*)ctx->aux3.ptr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(re, ctx->aux2.ptr, vb, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(im, ctx->aux3.ptr, vb, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return DH_OK;
 }
@@ -3134,7 +3183,7 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
                                         (int32_t*)A.bad, nullptr, st, A.live_count, true);
             if (e) return e;
             // a fused request stored its tile partials only (no hand-off): the step sums them
-            A.part_mode = !ctx->exact && ctx->last_path == DH_PATH_FUSED ? 1 : 0;
+            A.part_mode = !per_term(ctx, N) && ctx->last_path == DH_PATH_FUSED ? 1 : 0;
             A.part_sse = (const double*)ctx->part_sse.ptr;
             e = launch_lb_step(st, A, n_live);
             if (e) return e;
@@ -3443,12 +3492,21 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
         return fail(DH_E_ARG, "too many starts for one asynchronous request (use dh_surface_fg)");
     DeviceScope dev_scope(ctx->device);
     if (dev_scope.rc) return dev_scope.rc;
-    // the loss launch grows the context's device scratch (partials, counters, the prologue
-    // buffer, clamp workspaces) when this request has more tasks than any before; a grow frees
-    // the old buffers, so let the other slot's request finish first
+    // The loss launch may grow the context's device scratch (partials, counters, the prologue
+    // buffer, table / clamp workspaces), whose sizes follow from the surface, N and the param-set
+    // count only.  A grow frees buffers the other slot's enqueued launch still reads.  hipFree
+    // happens to synchronise the device first, but nothing here relies on that: wait for the
+    // other slot whenever this request is not covered by an earlier one on the same surface and
+    // N (the pipelined SciPy driver's requests always are, after its first two).
     auto& O = ctx->fg[1 - slot];
     const size_t units = P * (size_t)std::max(s->n_tiles, s->n_groups);
-    if (O.pending && units > ctx->fg_max_units) HIP_TRY(hipEventSynchronize(O.done));
+    const bool covered = s == ctx->fg_surf && N == ctx->fg_N && units <= ctx->fg_max_units;
+    if (O.pending && !covered) HIP_TRY(hipEventSynchronize(O.done));
+    if (s != ctx->fg_surf || N != ctx->fg_N) {
+        ctx->fg_surf = s;
+        ctx->fg_N = N;
+        ctx->fg_max_units = 0;
+    }
     ctx->fg_max_units = std::max(ctx->fg_max_units, units);
     HIP_TRY(F.h_params.reserve(P * DH_PARAM_STRIDE * 8));
     HIP_TRY(F.h_loss.reserve(P * 12));
@@ -3457,6 +3515,7 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     if (!F.done) HIP_TRY(hipEventCreateWithFlags(&F.done, hipEventDisableTiming));
     F.S = S;
     F.M = s->M;
+    F.surf = s;
     if (S == 0) {
         HIP_TRY(hipEventRecord(F.done, ctx->stream));
         F.pending = true;
@@ -3472,12 +3531,18 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     return DH_OK;
 }
 
-extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, double* f, double* g,
-                                 double* low) {
+extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, int S, double* f,
+                                 double* g, double* low) {
     if (!ctx || !s) return fail(DH_E_ARG, "null argument");
     if (slot < 0 || slot > 1) return fail(DH_E_ARG, "slot must be 0 or 1");
     auto& F = ctx->fg[slot];
     if (!F.pending) return fail(DH_E_ARG, "no request in flight in this slot");
+    // the slot belongs to the context: the caller must name the request it enqueued (its surface
+    // and start count, which size f / g / low), else its buffers may be smaller than F.S rows
+    if (s != F.surf) return fail(DH_E_ARG, "slot's request was enqueued on another surface");
+    if (S != F.S)
+        return fail(DH_E_ARG, "slot's request has " + std::to_string(F.S) + " starts, caller passed " +
+                                  std::to_string(S));
     if (F.S > 0 && (!f || !g || !low)) return fail(DH_E_ARG, "null argument");
     DeviceScope dev_scope(ctx->device);
     if (dev_scope.rc) return dev_scope.rc;
@@ -3493,6 +3558,18 @@ extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, dou
     const size_t P = (size_t)F.S * dhlb::kPts;
     fg_finish(F.S, F.M, (const double*)F.h_loss.ptr, (const int32_t*)((double*)F.h_loss.ptr + P),
               F.pen.data(), F.dx.data(), f, g, low);
+    return DH_OK;
+}
+
+extern "C" int dh_surface_fg_cancel(dh_ctx* ctx, int slot) {
+    if (!ctx) return fail(DH_E_ARG, "null argument");
+    if (slot < 0 || slot > 1) return fail(DH_E_ARG, "slot must be 0 or 1");
+    auto& F = ctx->fg[slot];
+    if (!F.pending) return DH_OK;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
+    F.pending = false;                  // cleared even if the wait fails: the slot is usable again
+    HIP_TRY(hipEventSynchronize(F.done));
     return DH_OK;
 }
 

@@ -22,7 +22,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DHCOS_LIB", os.path.join(_HERE, "libdhcos.so"))
 
 PARAM_STRIDE = 16
-MAX_N = 2048
+MAX_N = 2048                   # longest series of the table (fast) path (DH_MAX_N)
+MAX_N_PER_TERM = 65536         # longest accepted; longer than MAX_N runs the per-term path
 STRIKE_ABSOLUTE = 0
 STRIKE_PCT_SPOT = 1
 PATH_AUTO, PATH_SPLIT, PATH_FUSED = 0, 1, 2
@@ -88,9 +89,11 @@ SIGNATURES = {
                                 C.c_double, _vp, _vp, _vp]),
     "dh_surface_fg_begin": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, C.c_double, C.c_double,
                                       C.c_int, C.c_double, C.c_int]),
-    "dh_surface_fg_end": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, _vp]),
+    "dh_surface_fg_end": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _vp, _vp, _vp]),
+    "dh_surface_fg_cancel": (C.c_int, [_vp, C.c_int]),
     "dh_price_pairs": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp]),
     "dh_cf": (C.c_int, [_vp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
+    "dh_cf_complex": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int, C.c_double, _dp, _dp]),
     "dh_trunc_range": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int64, C.c_double, _dp, _dp]),
     "dh_cos_coeffs": (C.c_int, [_vp, _i32p, C.c_int, C.c_double, C.c_double, C.c_double,
                                 C.c_double, _dp, _dp]),
@@ -172,6 +175,9 @@ class Context:
         self._h = h
         self.device = int(device)
         self._lock = threading.Lock()
+        # the two request slots of dh_surface_fg_begin / _end belong to the context: the start
+        # count of the request in flight in each (None = idle), which sizes fg_end's outputs
+        self._fg_s = [None, None]
 
     @property
     def handle(self):
@@ -224,6 +230,14 @@ class Context:
 
     def synchronize(self):
         _check(load().dh_ctx_synchronize(self._h))
+
+    def fg_cancel(self, slot):
+        """dh_surface_fg_cancel: wait for slot's request (if any) and discard it."""
+        with self._lock:
+            try:
+                _check(load().dh_surface_fg_cancel(self._h, int(slot)))
+            finally:
+                self._fg_s[int(slot)] = None
 
     def close(self):
         if getattr(self, "_h", None):
@@ -297,6 +311,17 @@ class Context:
             _check(load().dh_cf(self._h, _ptr(p), _ptr(u), u.size, float(tau), _ptr(re), _ptr(im)))
         return re + 1j * im
 
+    def cf_complex(self, params16, u, tau):
+        """phi at complex frequencies u (dh_cf_complex)."""
+        p = _f64(params16).reshape(PARAM_STRIDE)
+        u = np.asarray(u, dtype=np.complex128).reshape(-1)
+        ur, ui = _f64(u.real), _f64(u.imag)
+        re, im = np.empty(u.size), np.empty(u.size)
+        with self._lock:
+            _check(load().dh_cf_complex(self._h, _ptr(p), _ptr(ur), _ptr(ui), u.size, float(tau),
+                                        _ptr(re), _ptr(im)))
+        return re + 1j * im
+
     def trunc_range(self, params, K, T, L=10.0):
         params = _f64(params).reshape(-1, PARAM_STRIDE)
         P = params.shape[0]
@@ -333,7 +358,6 @@ class Surface:
                                         C.byref(h)))
         self._h = h
         self.M = M
-        self._fg_s = [0, 0]              # starts of the request in each fg_begin slot
         m, nt = C.c_int32(0), C.c_int32(0)
         _check(load().dh_surface_size(h, C.byref(m), C.byref(nt)))
         self.n_tiles = nt.value
@@ -425,15 +449,18 @@ class Surface:
             _check(load().dh_surface_fg_begin(self.ctx.handle, self._h, X0.ctypes.data,
                                               None if model is None else model.ctypes.data, S,
                                               float(S0), float(r), int(N), float(L), int(slot)))
-        self._fg_s[slot] = S
+            self.ctx._fg_s[int(slot)] = S
 
     def fg_end(self, slot=0):
-        """dh_surface_fg_end: wait for slot's request -> (f [S], g [S, 13], low [S])."""
-        S = self._fg_s[slot]
-        f, g, low = np.empty(S), np.empty((S, 13)), np.empty(S)
+        """dh_surface_fg_end: wait for slot's request -> (f [S], g [S, 13], low [S]).  The slot
+        must hold a request this surface enqueued (the library checks the surface and S)."""
         with self.ctx._lock:
-            _check(load().dh_surface_fg_end(self.ctx.handle, self._h, int(slot), f.ctypes.data,
+            S = self.ctx._fg_s[int(slot)] if 0 <= int(slot) <= 1 else None
+            S = 0 if S is None else S          # an idle slot: the library reports the error
+            f, g, low = np.empty(S), np.empty((S, 13)), np.empty(S)
+            _check(load().dh_surface_fg_end(self.ctx.handle, self._h, int(slot), S, f.ctypes.data,
                                             g.ctypes.data, low.ctypes.data))
+            self.ctx._fg_s[int(slot)] = None
         return f, g, low
 
     # device-pointer variants (torch tensors or raw device addresses)
@@ -549,9 +576,11 @@ _tls = threading.local()
 
 def resolve_device(device: int | None = None) -> int:
     """The GPU a call without an explicit ``device=`` runs on, in this order: $DHCOS_DEVICE;
-    under torch.distributed (one process per GPU, e.g. torchrun) the rank's own GPU, i.e.
-    $LOCAL_RANK modulo the visible devices, else torch's current device; otherwise 0.
-    ``distributed._comm_device`` puts the collectives' tensors on the same GPU."""
+    under torch.distributed (one process per GPU, e.g. torchrun) torch's current device when
+    torch sees a GPU -- the device the rank bound with ``torch.cuda.set_device`` / the process
+    group's ``device_id``, whatever rank-to-GPU map the caller used -- else $LOCAL_RANK modulo the
+    visible devices; otherwise 0.  ``distributed._comm_device`` puts the collectives' tensors on
+    the same GPU."""
     if device is not None:
         return int(device)
     env = os.environ.get("DHCOS_DEVICE")
@@ -560,12 +589,12 @@ def resolve_device(device: int | None = None) -> int:
     torch = sys.modules.get("torch")
     dist = getattr(torch, "distributed", None) if torch is not None else None
     if dist is not None and dist.is_available() and dist.is_initialized():
+        if torch.cuda.is_available():
+            return int(torch.cuda.current_device())
         local = os.environ.get("LOCAL_RANK")
         if local not in (None, ""):
             n = device_count()
             return int(local) % n if n > 0 else int(local)
-        if torch.cuda.is_available():
-            return int(torch.cuda.current_device())
     return 0
 
 
@@ -582,6 +611,7 @@ def default_context(device: int | None = None) -> Context:
 
 
 __all__ = ["gen_draw", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
-           "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "STRIKE_ABSOLUTE",
+           "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "MAX_N_PER_TERM",
+           "STRIKE_ABSOLUTE",
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "LIB_PATH", "SIGNATURES",
            "Comm", "comm_id", "best_start", "COMM_ID_BYTES"]

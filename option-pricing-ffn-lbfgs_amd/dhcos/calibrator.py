@@ -127,12 +127,27 @@ def fd_models(X0, h=FD_ABS_STEP):
     return P.reshape(2, X0.shape[0], N_PARAMS)
 
 
+def _custom_loss(cal):
+    """True when a subclass replaces compute_loss or loss_batch: its losses must then be used
+    (the reference's minimize calls self.compute_loss), not the native request."""
+    cls = type(cal)
+    return (cls.compute_loss is not DoubleHestonJumpCalibrator.compute_loss
+            or cls.loss_batch is not DoubleHestonJumpCalibrator.loss_batch)
+
+
 def fg_from_losses(cal, X0):
-    """fg_batch through ``cal.loss_batch``: the 14 points of each request, their losses, SciPy's
+    """fg_batch through the calibrator's own losses (``compute_loss`` per point when a subclass
+    replaces it, else ``loss_batch``): the 14 points of each request, their losses, SciPy's
     forward difference and the smallest valid loss (NaN never wins, 1e10 is not valid)."""
     S = X0.shape[0]
     X, dx = fd_request_points_many(X0)
-    F = cal.loss_batch(X, track=False).reshape(S, N_PARAMS + 1)
+    custom = getattr(type(cal), "compute_loss", DoubleHestonJumpCalibrator.compute_loss)
+    if custom is not DoubleHestonJumpCalibrator.compute_loss and hasattr(cal, "market_options"):
+        n0 = cal.n_calls
+        F = np.array([cal.compute_loss(x) for x in X], dtype=np.float64).reshape(S, N_PARAMS + 1)
+        cal.n_calls = n0                # run_starts keeps the per-start counts
+    else:
+        F = cal.loss_batch(X, track=False).reshape(S, N_PARAMS + 1)
     G = (F[:, 1:] - F[:, :1]) / dx
     low = np.min(np.where((F == INVALID_LOSS) | np.isnan(F), np.inf, F), axis=1)
     return F[:, 0].copy(), G, low
@@ -251,7 +266,7 @@ class DoubleHestonJumpCalibrator:
         request; the transforms by NumPy, fd_models) unless a subclass replaces loss_batch,
         whose values are then used the same way."""
         X0 = np.atleast_2d(np.asarray(X0, dtype=np.float64))
-        native = type(self).loss_batch is DoubleHestonJumpCalibrator.loss_batch
+        native = not _custom_loss(self)
         surf = self._get_surface() if native and len(self.market_options) else None
         if surf is None:
             return fg_from_losses(self, X0)
@@ -473,8 +488,7 @@ def _pipeline_surface(cal, n_starts):
     cls = type(cal)
     if (not isinstance(cal, DoubleHestonJumpCalibrator)
             or cls.fg_batch is not DoubleHestonJumpCalibrator.fg_batch
-            or cls.loss_batch is not DoubleHestonJumpCalibrator.loss_batch
-            or not len(cal.market_options)):
+            or _custom_loss(cal) or not len(cal.market_options)):
         return None
     return cal._get_surface()
 
@@ -512,6 +526,31 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
     return outcomes
 
 
+def _fg(cal, X0):
+    return cal.fg_batch(X0) if hasattr(cal, "fg_batch") else fg_from_losses(cal, X0)
+
+
+def _fg_per_start(cal, ids, X0, gens, pending):
+    """A group request that raised (a subclass's loss): the reference runs each start in its own
+    try/except (lbfgs_calibrator.py:258-317), so only a start whose own request raises is dropped.
+    Re-evaluate the group's starts one at a time (a start's values do not depend on the batch),
+    drop the raising ones and return the survivors' (ids, f0, G, lows)."""
+    keep, rows = [], []
+    for j, sid in enumerate(ids):
+        try:
+            rows.append(_fg(cal, X0[j:j + 1]))
+            keep.append(sid)
+        except _native.NativeError:
+            raise
+        except Exception:              # noqa: BLE001 -- reference: except -> continue
+            gens[sid].close()
+            del pending[sid]
+    if not keep:
+        return keep, None, None, None
+    return (keep, np.concatenate([r[0] for r in rows]), np.concatenate([r[1] for r in rows]),
+            np.concatenate([r[2] for r in rows]))
+
+
 def _advance(cal, gens, states, order, outcomes):
     """run_starts' loop: one launch per lockstep request, setulb steps per start."""
     launches = 0
@@ -521,31 +560,17 @@ def _advance(cal, gens, states, order, outcomes):
             pending[sid] = next(gens[sid])
         while pending:
             ids = sorted(pending)
+            X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
             try:
-                X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
-                f0, G, lows = (cal.fg_batch(X0) if hasattr(cal, "fg_batch")
-                               else fg_from_losses(cal, X0))
+                f0, G, lows = _fg(cal, X0)
             except _native.NativeError:
                 raise
-            except Exception:          # reference: except -> continue (the start is dropped)
-                for sid in ids:
-                    gens[sid].close()
-                pending.clear()
-                break
+            except Exception:          # some start's loss raised: drop that start only
+                ids, f0, G, lows = _fg_per_start(cal, ids, X0, gens, pending)
+                if not ids:
+                    continue
             launches += 1
-            # per-start best valid loss (NaN never wins, 1e10 is not a valid loss)
-            for j, sid in enumerate(ids):
-                st = states[sid]
-                st.n_calls += N_PARAMS + 1
-                if lows[j] < st.best_loss:
-                    st.best_loss = lows[j]
-                try:
-                    pending[sid] = gens[sid].send((f0[j], G[j]))
-                except StopIteration as stop:
-                    outcomes[sid] = (stop.value, time.time())
-                    del pending[sid]
-                except Exception:      # noqa: BLE001 -- reference: except -> continue
-                    del pending[sid]
+            _consume(states, gens, pending, outcomes, ids, f0, G, lows)
     cal.lockstep_launches = launches
 
 
@@ -575,6 +600,7 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
     groups = [[s for s in range(n) if s % 2 == k] for k in (0, 1)]
     pending = {sid: next(gens[sid]) for sid in range(n)}
     inflight = [None, None]
+    busy = [False, False]              # slot k holds a request of this loop (fg_begin .. fg_end)
     launches = 0
 
     def submit(k):
@@ -585,26 +611,47 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
         X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
         try:
             model = fd_models(X0)
-        except Exception:          # reference: except -> continue (the starts are dropped)
-            for sid in ids:
-                gens[sid].close()
-                del pending[sid]
-            return
+        except Exception:          # reference: except -> continue, for the raising start only
+            keep = []
+            for j, sid in enumerate(ids):
+                try:
+                    fd_models(X0[j:j + 1])
+                    keep.append(j)
+                except Exception:  # noqa: BLE001
+                    gens[sid].close()
+                    del pending[sid]
+            if not keep:
+                return
+            ids, X0 = [ids[j] for j in keep], X0[keep]
+            model = fd_models(X0)
         cal.loss_evals += X0.shape[0] * (N_PARAMS + 1)
         surf.fg_begin(X0, cal.spot, cal.risk_free_rate, cal.N, model=model, slot=k)
         inflight[k] = ids
+        busy[k] = True
 
-    submit(0)
-    submit(1)
-    while inflight[0] is not None or inflight[1] is not None:
+    # the slots belong to the surface's context (the per-thread default context): whatever ends
+    # this loop -- an error, a KeyboardInterrupt -- must leave no request in flight in them
+    try:
+        submit(0)
+        submit(1)
+        while inflight[0] is not None or inflight[1] is not None:
+            for k in (0, 1):
+                ids = inflight[k]
+                if ids is None:
+                    continue
+                inflight[k] = None
+                f0, G, lows = surf.fg_end(k)
+                busy[k] = False
+                launches += 1
+                _consume(states, gens, pending, outcomes, ids, f0, G, lows)
+                submit(k)
+    finally:
         for k in (0, 1):
-            ids = inflight[k]
-            if ids is None:
-                continue
-            f0, G, lows = surf.fg_end(k)
-            launches += 1
-            _consume(states, gens, pending, outcomes, ids, f0, G, lows)
-            submit(k)
+            if busy[k]:
+                try:
+                    surf.ctx.fg_cancel(k)
+                except Exception:      # noqa: BLE001 -- unwinding: the first error wins
+                    pass
     cal.lockstep_launches = launches
 
 

@@ -54,9 +54,16 @@ class DoubleHeston:
 
     # -- reference API --------------------------------------------------------------------
     def characteristic_function(self, phi, tau):
-        """phi(u; tau) for real ``phi`` (scalar or array) -- double_heston.py:48-97."""
-        u = np.asarray(phi, dtype=np.float64)
-        vals = self._ctx().cf(self._record(), u.reshape(-1), tau)
+        """phi(u; tau) for real or complex ``phi`` (scalar or array) -- double_heston.py:48-97.
+        Real input takes the real-frequency kernel; complex input (any complex dtype, even with
+        a zero imaginary part) the complex-frequency one, as the reference's complex arithmetic."""
+        u = np.asarray(phi)
+        if np.iscomplexobj(u):
+            vals = self._ctx().cf_complex(self._record(), u.reshape(-1), tau)
+        elif u.dtype.kind in "biuf":
+            vals = self._ctx().cf(self._record(), u.astype(np.float64).reshape(-1), tau)
+        else:
+            raise TypeError(f"phi must be real or complex, got dtype {u.dtype}")
         return vals.reshape(u.shape) if u.ndim else np.complex128(vals[0])
 
     def truncationRange(self, L=10):

@@ -45,6 +45,12 @@ def gen_golden():
 
 
 @pytest.fixture(scope="session")
+def cf_complex_golden():
+    with open(os.path.join(GOLDEN, "cf_complex.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="session")
 def grid():
     with np.load(os.path.join(GOLDEN, "pricing_grid.npz")) as z:   # allow_pickle=False default
         return {k: z[k] for k in z.files}

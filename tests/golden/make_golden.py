@@ -11,6 +11,7 @@ evaluates them on seeded inputs and writes plain data files:
   calib.json          calibrator transforms, losses, one FD batch, minimize() and
                       calibrate() outcomes on the reference's own test market
   generator.json      generate_synthetic_calibrations() under np.random.seed(0)
+  cf_complex.json     characteristic_function at complex phi (scalars and one array)
 
 Reference call sites exercised (file:line in /root/reference):
   src/models/double_heston.py:48-97   characteristic_function
@@ -22,6 +23,7 @@ Reference call sites exercised (file:line in /root/reference):
   tests/test_suite.py:196-321 pricing sanity params and the calibration test market
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--skip-calibrate]
+                                                                       [--only-cf-complex]
 """
 import json
 import os
@@ -122,6 +124,30 @@ def kat():
             out["trunc"].append(dict(params=jumps, S0=100.0, K=K, T=T, r=0.03,
                                      a=f(a), b=f(b), a_L5=f(a5), b_L5=f(b5)))
     return out
+
+
+def cf_complex():
+    """characteristic_function at complex phi (double_heston.py:48-97 documents phi : complex):
+    the damped-integrand shifts u - i alpha used by Fourier pricers, upper-half-plane points, and
+    complex values with a zero imaginary part, as np.complex128 scalars and as one array."""
+    jumps = DEMO + [0.5, -0.05, 0.10]
+    other = [0.06, 3.1, 0.05, 0.45, -0.8, 0.03, 0.6, 0.06, 0.3, -0.25, 0.2, -0.06, 0.09]
+    rows = []
+    for p, r, q in ((jumps, 0.05, 0.0), (other, 0.03, 0.01)):
+        dh = make(100.0, 100.0, 1.0, r, p, "C", q)
+        for u in (0.0, 0.3, 1.0, 4.5, 20.0, 75.0):
+            for im in (-1.5, -1.0, -0.5, 0.0, 0.25, 1.0):
+                for tau in (0.1, 1.0, 2.5):
+                    c = complex(dh.characteristic_function(np.complex128(complex(u, im)), tau))
+                    rows.append(dict(params=p, r=r, q=q, re_phi=u, im_phi=im, tau=tau,
+                                     re=c.real, im=c.imag))
+    dh = make(100.0, 100.0, 1.0, 0.05, jumps, "C")
+    z = np.array([0.5 - 1.0j, 2.0 + 0.5j, 10.0 - 0.25j, 0.0 + 0.0j])
+    c = dh.characteristic_function(z, 0.7)
+    return {"points": rows,
+            "array": dict(params=jumps, r=0.05, q=0.0, tau=0.7, re_phi=list(map(f, z.real)),
+                          im_phi=list(map(f, z.imag)), re=list(map(f, c.real)),
+                          im=list(map(f, c.imag)))}
 
 
 def grid(n=1600, seed=1234):
@@ -266,6 +292,10 @@ def generator():
 def main():
     skip = "--skip-calibrate" in sys.argv
     t0 = time.time()
+    with open(os.path.join(OUT, "cf_complex.json"), "w") as fh:
+        json.dump(cf_complex(), fh, indent=1)
+    if "--only-cf-complex" in sys.argv:           # round 3: the complex-phi fixture alone
+        return
     with open(os.path.join(OUT, "kat.json"), "w") as fh:
         json.dump(kat(), fh, indent=1)
     print("kat done", time.time() - t0, flush=True)

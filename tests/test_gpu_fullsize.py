@@ -1,0 +1,242 @@
+"""Full-size GPU tests of the BASELINE configurations the north star is stated on.
+
+C3 (configs[2]): the 10,000-option surface (100 K/S in linspace(0.8, 1.2) x 100 T in
+linspace(0.1, 2.0), puts below the spot), N = 512, 3 starts x 14 forward-difference points = 42
+param sets per request -- the reference's compute_loss (lbfgs_calibrator.py:118-177) x 14 x 3 per
+lockstep request, each price double_heston.py:160-192.
+C4 (configs[3]): 64 starts on the 1,024-option C2 surface (32 x 32, calls, N = 256): 896 param
+sets = 28,672 tables per request, the fused kernel's prologue-kernel + 5-wave path.
+
+Tolerances (fp64): sampled prices vs the oracle 1e-10 relative (+1e-10 absolute, the bar's);
+the fast path vs the in-kernel reference-order path (exact mode) 1e-11 relative + 1e-11
+absolute over the whole grid; fused vs split bit for bit; loss sums vs the sums of the same
+kernel's prices 1e-12 relative.  Calibrations: property checks (trajectories are chaotic under
+last-bit noise, tests/test_calibration_sensitivity.py)."""
+import os
+import pickle
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import rel_close
+from oracle import dh_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GEN_LO = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
+GEN_HI = np.array([0.08, 4.5, 0.065, 0.5, -0.4, 0.07, 1.2, 0.07, 0.35, -0.2, 0.25, -0.01, 0.12])
+SCIPY_MESSAGES = ("CONVERGENCE: RELATIVE REDUCTION OF F <= FACTR*EPSMCH",
+                  "CONVERGENCE: NORM OF PROJECTED GRADIENT <= PGTOL", "ABNORMAL: ",
+                  "STOP: TOTAL NO. OF ITERATIONS REACHED LIMIT",
+                  "STOP: TOTAL NO. OF F,G EVALUATIONS EXCEEDS LIMIT")
+
+
+@pytest.fixture(scope="module")
+def dh():
+    import dhcos
+    from dhcos import _native
+    if _native.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return dhcos
+
+
+def surface(nK, nT, put_itm, N, S0=100.0, r=0.03):
+    """SURVEY 8(d)'s synthetic market (as bench.py's): model prices at a seed-1 draw x (1 +
+    N(0, 0.02)) with seed 2.  -> (market options, K, T, call, true params)."""
+    from dhcos import _native
+    kk, tt = np.meshgrid(np.linspace(0.8, 1.2, nK) * S0, np.linspace(0.1, 2.0, nT))
+    K, T = kk.ravel(), tt.ravel()
+    call = (K >= S0) if put_itm else np.ones(K.size, dtype=bool)
+    true = GEN_LO + (GEN_HI - GEN_LO) * np.random.RandomState(1).rand(13)
+    rec = np.zeros((1, 16))
+    rec[0, :13], rec[0, 13], rec[0, 14] = true, S0, r
+    model = _native.Surface(_native.default_context(), K, T, call).price(rec, N)[0]
+    mkt = model * (1 + np.random.RandomState(2).normal(0, 0.02, K.size))
+    opts = [{"strike": float(k), "maturity": float(t), "price": float(p),
+             "option_type": "call" if c else "put"} for k, t, p, c in zip(K, T, mkt, call)]
+    return opts, K, T, call, true
+
+
+def request_records(cal, starts, seed):
+    """[14 * starts, 16]: every start's function+gradient request around x0 + noise."""
+    from dhcos.calibrator import fd_request_points, x_to_model
+    rs = np.random.RandomState(seed)
+    x0 = cal.get_initial_guess(0)
+    X = np.concatenate([fd_request_points(x0 + rs.normal(0, 0.05, 13))[0] for _ in range(starts)])
+    rec = np.zeros((X.shape[0], 16))
+    rec[:, :13], rec[:, 13], rec[:, 14] = x_to_model(X), cal.spot, cal.risk_free_rate
+    return rec
+
+
+def _with_path(ctx, path, fn):
+    ctx.set_path(path)
+    try:
+        return fn()
+    finally:
+        ctx.set_path(0)
+
+
+def test_c3_request_full_size(dh):
+    """One C3 request (42 param sets x 10,000 options, N = 512) priced and reduced: sampled rows
+    against the oracle, the whole grid against exact mode, fused == split bit for bit, and the
+    loss sums equal to the sums of the same kernel's prices."""
+    from dhcos import _native
+    N = 512
+    opts, K, T, call, _ = surface(100, 100, True, N)
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.03, opts, N=N)
+    surf = cal._get_surface()
+    ctx = surf.ctx
+    rec = request_records(cal, 3, seed=7)
+    assert rec.shape == (42, 16) and surf.M == 10_000
+    res = {}
+    for path in (_native.PATH_SPLIT, _native.PATH_FUSED):
+        pr = _with_path(ctx, path, lambda: surf.price(rec, N))
+        sse, bad, lp = _with_path(ctx, path, lambda: surf.loss_terms(rec, N, want_prices=True))
+        res[path] = (pr, sse, bad, lp)
+    s, f = res[_native.PATH_SPLIT], res[_native.PATH_FUSED]
+    for a, b in zip(s, f):
+        assert np.array_equal(a, b), np.max(np.abs(np.asarray(a, float) - np.asarray(b, float)))
+    prices, sse, bad = f[0], f[1], f[2]
+    assert np.array_equal(prices, f[3])
+    assert np.isfinite(prices).all() and (bad == 0).all()
+    mkt = cal.market_prices
+    assert rel_close(sse, np.sum(((prices - mkt) / mkt) ** 2, axis=1), 1e-12, 0).all()
+    # the request the calibrator forms from the same records: sse / M + Feller
+    rs = np.random.RandomState(3)
+    for p in (0, 20, 41):
+        idx = np.sort(rs.choice(surf.M, 150, replace=False))
+        want = O.price_many(rec[p, :13], 100.0, K[idx], T[idx], 0.03, call[idx], N)
+        assert rel_close(prices[p, idx], want, 1e-10, 1e-10).all(), \
+            np.max(np.abs(prices[p, idx] - want) / np.abs(want))
+    ctx.set_exact(True)
+    try:
+        exact = surf.price(rec, N)
+    finally:
+        ctx.set_exact(False)
+    err = np.abs(prices - exact)
+    assert (err <= 1e-11 * np.abs(exact) + 1e-11).all(), err.max()
+    print("C3 fast vs exact: max abs", err.max(), "max rel", np.max(err / np.abs(exact)))
+
+
+@pytest.mark.parametrize("driver", ["scipy", "device"])
+def test_c3_calibrate_three_starts(dh, driver):
+    """calibrate(300, 3) on the C3 surface under np.random.seed(0), both optimizer drivers:
+    a SciPy message, iterations within maxiter, the winner below the best start's own initial
+    loss, the re-priced model prices equal to the
+    surface's prices at the winning parameters, and (for a converged winner) the final loss
+    equal to the loss of those prices."""
+    N = 512
+    opts, K, T, call, _ = surface(100, 100, True, N)
+    np.random.seed(0)
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.03, opts, N=N)
+    x0s = cal.start_points(3)
+    start_loss = [cal.compute_loss(x) for x in x0s]
+    res = cal.calibrate(maxiter=300, x0s=x0s, driver=driver)
+    assert res.message in SCIPY_MESSAGES and 0 <= res.iterations <= 300
+    assert np.isfinite(res.final_loss) and res.final_loss < min(start_loss)
+    prm = np.array([res.parameters[n] for n in cal.param_names])
+    rec = np.zeros((1, 16))
+    rec[0, :13], rec[0, 13], rec[0, 14] = prm, 100.0, 0.03
+    assert np.array_equal(res.model_prices, cal._get_surface().price(rec, N)[0])
+    if res.message.startswith("CONVERGENCE"):
+        x = cal.inverse_transform_params(res.parameters)
+        assert rel_close(cal.compute_loss(x), res.final_loss, 1e-6, 0)
+    print(driver, res.final_loss, res.iterations, res.message, "starts", start_loss)
+
+
+def test_c4_request_fused_split_bitwise(dh):
+    """A C4 request: 64 starts x 14 points = 896 param sets on the C2 surface (28,672 tables:
+    table_prologue_kernel + the 5-wave fused build) equals the split path bit for bit, and
+    sampled rows the oracle."""
+    from dhcos import _native
+    N = 256
+    opts, K, T, call, _ = surface(32, 32, False, N)
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.03, opts, N=N)
+    surf = cal._get_surface()
+    ctx = surf.ctx
+    rec = request_records(cal, 64, seed=8)
+    assert rec.shape[0] * 32 == 28_672
+    out = {}
+    for path in (_native.PATH_SPLIT, _native.PATH_FUSED):
+        sse, bad, pr = _with_path(ctx, path, lambda: surf.loss_terms(rec, N, want_prices=True))
+        out[path] = (sse, bad, pr)
+    for a, b in zip(out[_native.PATH_SPLIT], out[_native.PATH_FUSED]):
+        assert np.array_equal(a, b)
+    pr = out[_native.PATH_FUSED][2]
+    rs = np.random.RandomState(4)
+    for p in (0, 447, 895):
+        idx = np.sort(rs.choice(surf.M, 100, replace=False))
+        want = O.price_many(rec[p, :13], 100.0, K[idx], T[idx], 0.03, call[idx], N)
+        assert rel_close(pr[p, idx], want, 1e-10, 1e-10).all()
+
+
+@pytest.mark.parametrize("driver", ["scipy", "device"])
+def test_c4_calibrate_64_starts(dh, driver):
+    """calibrate(300, 64) on the C2 surface on one GPU (C4's starts, unsharded): the winner is
+    the first start (in start order) with the smallest loss among the per-start outcomes, and
+    lockstep / pipelined / device batching of 64 starts changes no start's result."""
+    from dhcos.calibrator import run_starts, run_starts_device
+    N = 256
+    opts, K, T, call, _ = surface(32, 32, False, N)
+    np.random.seed(0)
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.03, opts, N=N)
+    x0s = cal.start_points(64)
+    res = cal.calibrate(maxiter=300, x0s=x0s, driver=driver)
+    runs = run_starts(cal, x0s, 300) if driver == "scipy" else run_starts_device(cal, x0s, 300)
+    funs = [r.fun if r.fun == r.fun else np.inf for r, _ in runs]   # NaN never wins
+    best = int(np.argmin(funs))                       # argmin: the first of equal minima
+    assert res.final_loss == funs[best] and res.iterations == runs[best][0].nit
+    assert res.message in SCIPY_MESSAGES
+    if driver == "scipy":                             # 64 starts in one lockstep launch each
+        seq = run_starts(cal, x0s[:8], 300, lockstep=True, pipeline=False)
+        for (a, _), (b, _) in zip(seq, runs[:8]):
+            assert np.array_equal(a.x, b.x) and a.fun == b.fun and a.nit == b.nit
+    else:
+        sub = run_starts_device(cal, x0s[:8], 300)
+        for (a, _), (b, _) in zip(sub, runs[:8]):
+            assert np.array_equal(a.x, b.x) and a.fun == b.fun and a.nit == b.nit
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _c4_rank(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dhcos
+        from dhcos import distributed as D
+        opts, *_ = surface(32, 32, False, 256)
+        np.random.seed(0 if rank == 0 else 77)
+        cal = dhcos.DoubleHestonJumpCalibrator(100.0, 0.03, opts, N=256)
+        res = D.calibrate_sharded(cal, maxiter=300, multi_start=64)
+        with open(os.path.join(out_dir, f"c4_{rank}.pkl"), "wb") as fh:
+            pickle.dump({"loss": res.final_loss, "nit": res.iterations, "msg": res.message,
+                         "params": res.parameters, "prices": res.model_prices,
+                         "stats": (cal.n_calls, cal.best_loss), "rng": np.random.rand()}, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c4_sharded_two_ranks_equals_single_process(dh, tmp_path):
+    """C4's sharding (calibrate_sharded: start s on rank s % world, one all-gather of the
+    per-start records, the reference's strict-< choice) with two gloo ranks sharing the box's
+    GPU: every rank returns single-process calibrate(300, 64)'s result, counters and RNG state."""
+    mp.spawn(_c4_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    opts, *_ = surface(32, 32, False, 256)
+    np.random.seed(0)
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.03, opts, N=256)
+    want = cal.calibrate(maxiter=300, multi_start=64)
+    stats, rng = (cal.n_calls, cal.best_loss), np.random.rand()
+    for r in range(2):
+        g = pickle.load(open(tmp_path / f"c4_{r}.pkl", "rb"))
+        assert g["loss"] == want.final_loss and g["nit"] == want.iterations
+        assert g["msg"] == want.message and g["params"] == want.parameters
+        np.testing.assert_array_equal(g["prices"], want.model_prices)
+        assert g["stats"] == stats and g["rng"] == rng

@@ -196,7 +196,31 @@ def test_empty_and_degenerate_sizes(dh):
     with pytest.raises(_native.NativeError):
         ctx.price_pairs(np.zeros((1, 16)), [100.0], [1.0], [1], N=0)
     with pytest.raises(_native.NativeError):
-        ctx.price_pairs(np.zeros((1, 16)), [100.0], [1.0], [1], N=_native.MAX_N + 1)
+        ctx.price_pairs(np.zeros((1, 16)), [100.0], [1.0], [1], N=_native.MAX_N_PER_TERM + 1)
+
+
+def test_long_series_per_term_path(dh):
+    """N beyond the fast path's LDS table (DH_MAX_N = 2048) runs the per-term path (the
+    reference's operation order, cos_exact_kernel): the reference's pricing(N) accepts any N.
+    Pairs, surfaces, loss sums and DoubleHeston.pricing at N = 2049 / 3000 / 4096 against the
+    oracle at the fidelity tolerance; the loss equals the sums of its own prices."""
+    from dhcos import _native
+    ctx = _native.default_context()
+    params, rec, K, T, call = _surface_case(61, P=2, M=40, n_T=4, N=4096)
+    mkt = np.abs(O.price_many(params[0], 100.0, K, T, 0.03, call, 128)) + 1e-3
+    surf = _native.Surface(ctx, K, T, call, mkt)
+    for N in (2049, 3000, 4096):
+        want = np.stack([O.price_many(params[p], 100.0, K, T, 0.03, call, N) for p in range(2)])
+        got = surf.price(rec, N)
+        assert rel_close(got, want, FID_RTOL, BAR_ATOL).all(), (N, np.abs(got - want).max())
+        pairs = ctx.price_pairs(np.repeat(rec[:1], 40, 0), K, T, call, N)
+        assert rel_close(pairs, want[0], FID_RTOL, BAR_ATOL).all()
+        sse, bad, pr = surf.loss_terms(rec, N, want_prices=True)
+        assert np.array_equal(pr, got)
+        assert rel_close(sse, np.sum(((got - mkt) / mkt) ** 2, axis=1), 1e-12, 0).all()
+    m = dh.DoubleHeston(100.0, K[0], T[0], 0.03, *params[0], option_type="C" if call[0] else "P")
+    assert rel_close(m.pricing(N=3000), O.price_many(params[0], 100.0, K[:1], T[:1], 0.03,
+                                                     call[:1], 3000)[0], FID_RTOL, BAR_ATOL)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -383,6 +407,92 @@ def test_fg_begin_end_slots(dh, calib_golden):
         want = surf.fg(Xi, 100.0, 0.05, 128, model=fd_models(Xi))
         for u, v in zip(got, want):
             assert np.array_equal(u, v)
+
+
+def test_characteristic_function_complex_phi(dh, cf_complex_golden):
+    """DoubleHeston.characteristic_function at complex phi (double_heston.py:48-61 documents
+    phi : complex) against the reference's values: 216 scalar points (damped shifts u - i alpha,
+    upper half plane, zero imaginary parts) and one array, within 1e-12 relative (complex
+    division / log / sqrt in another operation order than NumPy's).  Real input keeps the real
+    path; a non-numeric phi is a TypeError, never a silently dropped imaginary part."""
+    errs = []
+    for e in cf_complex_golden["points"]:
+        m = dh.DoubleHeston(100.0, 100.0, 1.0, e["r"], *e["params"], q=e["q"])
+        got = m.characteristic_function(np.complex128(complex(e["re_phi"], e["im_phi"])), e["tau"])
+        want = complex(e["re"], e["im"])
+        assert isinstance(got, np.complex128)
+        errs.append(abs(got - want) / abs(want))
+        assert abs(got - want) <= 1e-12 * abs(want), (e, got, want)
+    a = cf_complex_golden["array"]
+    m = dh.DoubleHeston(100.0, 100.0, 1.0, a["r"], *a["params"], q=a["q"])
+    z = np.array(a["re_phi"]) + 1j * np.array(a["im_phi"])
+    got = m.characteristic_function(z, a["tau"])
+    want = np.array(a["re"]) + 1j * np.array(a["im"])
+    assert got.shape == z.shape and np.all(np.abs(got - want) <= 1e-12 * np.abs(want))
+    real = m.characteristic_function(np.array([0.5, 2.0]), a["tau"])
+    cz = m.characteristic_function(np.array([0.5, 2.0]) + 0j, a["tau"])
+    assert np.all(np.abs(real - cz) <= 1e-13 * np.abs(cz))
+    with pytest.raises(TypeError):
+        m.characteristic_function(np.array(["x"]), 1.0)
+    print("complex-phi CF max rel err", max(errs))
+
+
+def test_fg_slots_belong_to_the_context(dh, calib_golden):
+    """The two request slots are the context's: fg_end from another surface of the same context,
+    or with another start count, is refused (the request stays in flight, the caller's buffers are
+    never overrun); fg_cancel discards a request and frees its slot."""
+    from dhcos import _native
+    from dhcos.calibrator import fd_models
+    g = calib_golden
+    cal_a = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    cal_b = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"][:4])
+    sa, sb = cal_a._get_surface(), cal_b._get_surface()
+    assert sa.ctx is sb.ctx
+    X = np.array([s["x0"] for s in g["calibrate_seed0_starts"]], dtype=float)
+    sa.fg_begin(X, 100.0, 0.05, 128, model=fd_models(X), slot=0)
+    with pytest.raises(_native.NativeError, match="another surface"):
+        sb.fg_end(0)
+    f, gg, low = np.empty(1), np.empty((1, 13)), np.empty(1)     # one row: too small for 3
+    lib = _native.load()
+    rc = lib.dh_surface_fg_end(sa.ctx.handle, sa.handle, 0, 1, f.ctypes.data, gg.ctypes.data,
+                               low.ctypes.data)
+    assert rc == -1 and b"3 starts" in lib.dh_last_error()
+    got = sa.fg_end(0)                                    # still in flight, still the same bits
+    want = sa.fg(X, 100.0, 0.05, 128, model=fd_models(X))
+    for u, v in zip(got, want):
+        assert np.array_equal(u, v)
+    sa.fg_begin(X, 100.0, 0.05, 128, model=fd_models(X), slot=1)
+    sa.ctx.fg_cancel(1)
+    sa.ctx.fg_cancel(1)                                   # idle: no-op
+    with pytest.raises(_native.NativeError):
+        sa.fg_end(1)
+    sa.fg_begin(X, 100.0, 0.05, 128, model=fd_models(X), slot=1)   # the slot is free again
+    for u, v in zip(sa.fg_end(1), want):
+        assert np.array_equal(u, v)
+
+
+def test_pipelined_driver_interrupted_leaves_context_usable(dh, calib_golden, monkeypatch):
+    """An interrupt inside the two-group pipeline (here: a KeyboardInterrupt from the per-request
+    transforms while the other group's request is in flight) must not leave a slot busy on the
+    thread's cached context: the next calibrate on it runs and gives the uninterrupted result."""
+    import dhcos.calibrator as CM
+    g = calib_golden
+    x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
+    want = CM.run_starts(dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"]), x0s, 300)
+    real, calls = CM.fd_models, [0]
+
+    def flaky(X0, *a, **k):
+        calls[0] += 1
+        if calls[0] == 5:
+            raise KeyboardInterrupt
+        return real(X0, *a, **k)
+    monkeypatch.setattr(CM, "fd_models", flaky)
+    with pytest.raises(KeyboardInterrupt):
+        CM.run_starts(dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"]), x0s, 300)
+    monkeypatch.setattr(CM, "fd_models", real)
+    got = CM.run_starts(dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"]), x0s, 300)
+    for (a, _), (b, _) in zip(got, want):
+        assert np.array_equal(a.x, b.x) and a.fun == b.fun and a.nit == b.nit
 
 
 def test_generator_matches_reference(dh, gen_golden, tmp_path):

@@ -95,5 +95,6 @@ def test_comm_and_async_fg_arguments_are_rejected():
     best = C.c_int32(7)
     assert lib.dh_allgather_best(None, None, 1, 3, 0, 1, None, C.byref(best)) == -1
     assert lib.dh_surface_fg_begin(None, None, None, None, 1, 100.0, 0.05, 128, 10.0, 0) == -1
-    assert lib.dh_surface_fg_end(None, None, 0, None, None, None) == -1
+    assert lib.dh_surface_fg_end(None, None, 0, 0, None, None, None) == -1
+    assert lib.dh_surface_fg_cancel(None, 0) == -1
     assert b"null" in lib.dh_last_error()
