@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "dh_exp_table.h"
 #include "dh_logatan_table.h"
 #include "dh_sincos_table.h"
 
@@ -116,13 +117,20 @@ __device__ __forceinline__ void dsincos(double x, double* sp, double* cp) {
 // copy of kSinCosPi64 (one ds_read_b128; correctly rounded entries), sin r and cos r by Taylor
 // polynomials through r^7 / r^8 (the next terms are < 1e-18 relative), then the angle-addition
 // formulas.  ~1 ulp for |x| < 2^20; 17 VALU instructions against dsincos's 41.
+// Table lookups of the CF loop round their index with the 1.5 * 2^52 shift: qd = fma(x, c, shift)
+// is shift + rint(x c) (its ulp is 1) and the low word of qd holds rint(x c) as a two's-
+// complement integer, so the index needs no float-to-int conversion (a NaN x gives a defined
+// index, masked in range, and a NaN result).  q = qd - shift is exact.
+constexpr double kShift52 = 0x1.8p52;
+
 __device__ __forceinline__ void dsincos_t(double x, const double2* __restrict__ tab, double* sp,
                                           double* cp) {
-    const double q = rint(x * 20.371832715762604);                    // x * 64/pi
+    const double qd = fma(x, 20.371832715762604, kShift52);          // rint(x 64/pi)
+    const double q = qd - kShift52;
     double r = fma(-q, 0.04908738521234052, x);                        // pi/64, 3 parts
     r = fma(-q, 1.9135106236677394e-18, r);
     r = fma(-q, -4.6793278276849057e-35, r);
-    const double2 sc = tab[(int)q & 127];                              // sin, cos (q pi/64)
+    const double2 sc = tab[__double2loint(qd) & 127];                  // sin, cos (q pi/64)
     const double z = r * r;
     double ps = fma(z, -0.0001984126984126984, 0.008333333333333333);
     ps = fma_k(z, ps, -0.16666666666666666);
@@ -293,13 +301,14 @@ __device__ __forceinline__ double datan2(double y, double x) {
     return (isnan(x) || isnan(y)) ? x + y : a;
 }
 
-// ---- table-driven log and atan2 of the CF loop ----------------------------------------------
+// ---- table-driven log, atan2 and exp of the CF loop --------------------------------------------
 // The CF's math tables in one LDS array of double2 (load_math_tables): [0, 128) sin / cos of
 // j pi/64 (dsincos_t), [128, 256) (invc, logc) of dlog_t, [256, 321) atan(j/64) (hi, lo) of
-// datan2_t.
+// datan2_t, [321, 385) 2^(j/64) (hi, lo) of dexp_t.
 constexpr int kTabLog = 128;
 constexpr int kTabAtan = 256;
-constexpr int kMathTab = 321;
+constexpr int kTabExp = 321;
+constexpr int kMathTab = 385;
 
 // log(x) for normal x > 0 (glibc's table layout, tools/gen_logatan_tables.py): x = 2^k z with z
 // in [0.6875, 1.375) from the bits, subinterval i by the next 7 bits, r = z invc_i - 1 (one FMA,
@@ -307,12 +316,13 @@ constexpr int kMathTab = 321;
 // (remainder < 2^-67).  Absolute error ~1 ulp of the result's scale (no special path near 1,
 // where only absolute accuracy matters here).  ~20 VALU against dlog's ~40.
 __device__ __forceinline__ double dlog_t(double x, const double2* __restrict__ tab) {
-    const long long ix = __double_as_longlong(x);
-    const long long tmp = ix - 0x3fe6000000000000LL;
-    const int i = (int)((tmp >> 45) & 127);
-    const double kd = (double)(int)(tmp >> 52);
-    const double z = __longlong_as_double(ix - (tmp & (0xfffLL << 52)));
-    const double2 e = tab[kTabLog + i];                              // (invc, logc)
+    // glibc's 64-bit integer steps on the high word only (the constant's low word is 0, so the
+    // subtraction never borrows): tmp = hi(x) - 0x3fe60000, i = tmp >> 13 & 127, k = tmp >> 20
+    const int hx = __double2hiint(x);
+    const int tmp = hx - 0x3fe60000;
+    const double kd = (double)(tmp >> 20);
+    const double z = __hiloint2double(hx - (tmp & (int)0xfff00000), __double2loint(x));
+    const double2 e = tab[kTabLog + ((tmp >> 13) & 127)];            // (invc, logc)
     const double r = fma(z, e.x, -1.0);
     const double w = fma(kd, 0x1.62e42fefa3800p-1, e.y);             // k ln2_hi exact (|k| < 2^11)
     const double hi = w + r;
@@ -339,21 +349,53 @@ __device__ __forceinline__ double datan2_t(double y, double x, const double2* __
     const double ax = fabs(x), ay = fabs(y);
     const double mx = fmax(ax, ay), mn = fmin(ax, ay);
     const double t0 = mn * __builtin_amdgcn_rcp(mx);
-    // 0 .. 64; clamped in fp so a NaN t0 (NaN operands, or D conj(d) = 0) indexes entry 0
-    // instead of converting NaN to int (poison) -- a NaN there already makes the price NaN
-    const int j = (int)fmin(fmax(rint(t0 * 64.0), 0.0), 64.0);
-    const double sj = (double)j * 0.015625;
+    // j = rint(64 t0) in 0 .. 64 by the shift (kShift52): a NaN t0 (NaN operands, or D conj(d) =
+    // 0) gives a defined index <= 127 (an entry of the next table) and a NaN result, never a NaN
+    // converted to int
+    const double qd = fma(t0, 64.0, kShift52);
+    const double sj = (qd - kShift52) * 0.015625;                     // j / 64, exact
     const double xp = fma(mn, sj, mx), yp = fma(-mx, sj, mn);
     const double tp = yp * drcp(xp);
     const double z = tp * tp;
     double q = fma(z, -0.14285714285714285, 0.2);
     q = fma_k(z, q, -0.3333333333333333);
     const double at = fma(tp * z, q, tp);
-    const double2 e = tab[kTabAtan + j];                             // atan(j/64) hi, lo
+    const double2 e = tab[kTabAtan + (__double2loint(qd) & 127)];    // atan(j/64) hi, lo
     double a = e.x + (at + e.y);
     a = (ay > ax) ? (1.57079632679489655800e+00 - a) + 6.12323399573676588613e-17 : a;
     a = signbit(x) ? (3.14159265358979311600e+00 - a) + 1.22464679914735317720e-16 : a;
     return copysign(a, y);
+}
+
+// exp(x) by a 64-entry table (glibc's layout, tools/gen_exp_table.py): x = (64 e + j) ln2/64 + r
+// with |r| <= ln2/128, q = 64 e + j rounded by the 1.5 * 2^52 shift (its low word IS q, so no
+// float-to-int conversion: a NaN x indexes a defined entry and stays NaN through r), e^r - 1 by
+// its Taylor series through r^5 (remainder < 4e-17 relative), then 2^e (hi + (hi (e^r - 1) + lo))
+// with 2^(j/64) = hi + lo.  ~1 ulp; 12 fp64 VALU against dexp's 19.  Finite x <= 709 (the CF's
+// exponents); callers select the overflow / underflow ends.
+__device__ __forceinline__ double dexp_t_core(double x, const double2* __restrict__ tab) {
+    const double qd = fma(x, 0x1.71547652b82fep+6, kShift52);        // rint(x 64/ln2)
+    const double q = qd - kShift52;
+    const int qi = __double2loint(qd);                                // q as int32
+    double r = fma(q, -0x1.62e42fefa39efp-7, x);                      // ln2/64, 2 parts
+    r = fma(q, -0x1.abc9e3b39803fp-62, r);
+    const double2 t = tab[kTabExp + (qi & 63)];                       // 2^(j/64): hi, lo
+    double p = fma(r, 0.008333333333333333, 0.041666666666666664);
+    p = fma_k(r, p, 0.16666666666666666);
+    p = fma_k(r, p, 0.5);
+    const double em1 = fma(r * r, p, r);                              // e^r - 1
+    return ldexp(t.x + fma(t.x, em1, t.y), qi >> 6);
+}
+
+__device__ __forceinline__ double dexp_t(double x, const double2* __restrict__ tab) {
+    const double e = dexp_t_core(x, tab);
+    return (x > 709.8) ? INFINITY : ((x < -1075.0) ? 0.0 : e);
+}
+
+// dexp_t for x <= 0 (or -inf / NaN): the CF's e^{-Re(d) tau} and Gaussian jump factor.
+__device__ __forceinline__ double dexp_t_nonpos(double x, const double2* __restrict__ tab) {
+    const double e = dexp_t_core(x, tab);
+    return (x < -1075.0) ? 0.0 : e;
 }
 
 // z1 / z2 through one reciprocal of |z2|^2 (no Smith scaling: |z2| on this path stays far
@@ -497,7 +539,7 @@ __device__ __forceinline__ cplx factor_x(const FactorC& F, double u, double tau,
     const cplx bp = {beta.re + dre, beta.im + dim};
     double es, ec;
     dsincos_t(-dim * tau, sct, &es, &ec);
-    const double em = dexp_nonpos(-dre * tau);
+    const double em = dexp_t_nonpos(-dre * tau, sct);
     const cplx e = {em * ec, em * es};
     const cplx D = {bp.re - (bm.re * e.re - bm.im * e.im), bp.im - (bm.re * e.im + bm.im * e.re)};
     const cplx ome = {1.0 - e.re, -e.im};
@@ -536,7 +578,7 @@ __device__ __forceinline__ cplx jump_x(const CfConsts& C, double u,
                                        const double2* __restrict__ sct) {
     double js, jc;
     dsincos_t(u * C.muj, sct, &js, &jc);
-    const double jm = dexp_nonpos(-(C.half_sj2 * (u * u)));
+    const double jm = dexp_t_nonpos(-(C.half_sj2 * (u * u)), sct);
     return {C.lt * (jm * jc - 1.0), C.lt * (jm * js)};
 }
 
@@ -549,7 +591,7 @@ __device__ __forceinline__ double cf_phase_from(const CfConsts& C, double u, dou
     E = cadd(E, J);
     double ps, pc;
     dsincos_t(E.im - u * a, sct, &ps, &pc);
-    return dexp(E.re) * pc;
+    return dexp_t(E.re, sct) * pc;
 }
 
 // Re(phi(u) e^{-i u a}) via the exponent form, one lane per entry; sct = LDS copy of kSinCosPi64
@@ -568,7 +610,8 @@ __device__ __forceinline__ void load_math_tables(double2* sct, int t_first) {
         if (i < 0) break;
         const double* src = i < kTabLog ? kSinCosPi64 + 2 * i
                           : (i < kTabAtan ? kLogInvcLogc + 2 * (i - kTabLog)
-                                          : kAtanJ64 + 2 * (i - kTabAtan));
+                          : (i < kTabExp ? kAtanJ64 + 2 * (i - kTabAtan)
+                                         : kExp2J64 + 2 * (i - kTabExp)));
         sct[i] = make_double2(src[0], src[1]);
     }
 }

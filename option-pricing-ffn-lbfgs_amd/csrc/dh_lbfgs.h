@@ -8,6 +8,12 @@
 // pair memory is a separate type R (LDS-resident on the device) with s(j), y(j), rho(j) (1 / dr),
 // a(j) (the two-loop's alpha scratch), put(j, s, y, rho) and shift() (drop the oldest pair).
 //
+// Attribution: the algorithm restated here is L-BFGS-B 3.0 (Ciyou Zhu, Richard Byrd, Jorge Nocedal,
+// Jose Luis Morales; BSD-3-Clause, as distributed with SciPy) and its MINPACK-2 line search
+// dcsrch / dcstep (Brett M. Averick, Jorge J. More; MINPACK-2 license, BSD-style), both via SciPy's
+// C translation (scipy/optimize/_lbfgsb, BSD-3-Clause).  No source text is copied; the logic is
+// restated for a wave-parallel state machine.
+//
 // What it restates (SciPy 1.15.3, the optimizer the reference calls at lbfgs_calibrator.py:259-269
 // as minimize(method='L-BFGS-B', options={maxiter, ftol: 1e-9, gtol: 1e-6}) without bounds):
 //   * the driver loop of scipy/optimize/_lbfgsb_py.py:_minimize_lbfgsb (:410-470) with

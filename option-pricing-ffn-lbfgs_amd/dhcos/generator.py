@@ -43,11 +43,42 @@ RISK_FREE = 0.03                                   # :94
 ALPHA = 0.9                                        # :108
 
 
-def trading_dates(n):
-    """Weekdays from 2022-01-03 as 'YYYY-MM-DD' (synthetic_generator.py:59-67): the reference's
-    weekend-skipping loop, as one NumPy business-day offset (same strings, 12x faster at 1M)."""
+def _civil(z):
+    """Proleptic Gregorian (year, month, day) of day numbers z since 1970-01-01 (H. Hinnant's
+    days-to-civil algorithm, vectorised in int64)."""
+    z = z + 719468
+    era = np.floor_divide(z, 146097)
+    doe = z - era * 146097
+    yoe = (doe - doe // 1460 + doe // 36524 - doe // 146096) // 365
+    doy = doe - (365 * yoe + yoe // 4 - yoe // 100)
+    mp = (5 * doy + 2) // 153
+    d = doy - (153 * mp + 2) // 5 + 1
+    m = np.where(mp < 10, mp + 3, mp - 9)
+    return yoe + era * 400 + (m <= 2), m, d
+
+
+def trading_dates_array(n):
+    """Weekdays from 2022-01-03 as a '<U10' array of 'YYYY-MM-DD' (synthetic_generator.py:59-67):
+    the reference's weekend-skipping loop as one NumPy business-day offset, formatted by integer
+    arithmetic into the code points of a U10 array (np.datetime_as_string's per-element
+    formatting was most of a 1M-sample run's host time; the strings are the same)."""
     days = np.busday_offset("2022-01-03", np.arange(int(n)), roll="forward")
-    return np.datetime_as_string(days, unit="D").tolist()
+    if days.size == 0:
+        return days.astype("U10")
+    y, m, d = _civil(days.astype(np.int64))
+    if y[-1] > 9999:                               # 5-digit years: NumPy's own formatting
+        return np.datetime_as_string(days, unit="D")
+    c = np.empty((days.size, 10), np.uint32)
+    c[:, 0], c[:, 1], c[:, 2], c[:, 3] = y // 1000, y // 100 % 10, y // 10 % 10, y % 10
+    c[:, 5], c[:, 6], c[:, 8], c[:, 9] = m // 10, m % 10, d // 10, d % 10
+    c += ord("0")
+    c[:, 4] = c[:, 7] = ord("-")
+    return c.view("U10").ravel()
+
+
+def trading_dates(n):
+    """trading_dates_array as a list of Python strings (the reference's per-record dates)."""
+    return trading_dates_array(n).tolist()
 
 
 def draw_paths(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
@@ -124,7 +155,9 @@ def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose
     say("GENERATING SYNTHETIC HISTORICAL CALIBRATIONS (MI355X batch path)")
     say("=" * 70)
     say(f"  samples: {n_samples}   save path: {save_path}   COS terms: {N}")
-    dates = trading_dates(n_samples)
+    # the columnar output keeps the dates as one '<U10' array: 10^6 Python strings were most of
+    # the host time of a 1M-sample run (profiles/r03_generator_e2e.json)
+    dates = trading_dates_array(n_samples) if as_arrays else trading_dates(n_samples)
     market = model + noise * model                                   # (:141-142)
     rel = (model - market) / market
     losses = np.mean(rel ** 2, axis=1)                               # (:154-157)
@@ -132,7 +165,7 @@ def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose
     Krel = np.tile(STRIKES_PCT, len(MATURITIES))
     Tg = np.repeat(MATURITIES, len(STRIKES_PCT))
     if as_arrays:
-        result = dict(dates=np.array(dates), spot=spots, risk_free=RISK_FREE, params=params,
+        result = dict(dates=dates, spot=spots, risk_free=RISK_FREE, params=params,
                       param_names=names, market_prices=market, model_prices=model,
                       strikes=(Krel[None, :] * spots[:, None]) / 100.0,
                       maturities=Tg, final_loss=losses)

@@ -72,3 +72,14 @@ def test_trading_dates_match_reference_loop():
     for n in (0, 1, 5, 6, 7, 11, 2500):
         got = G.trading_dates(n)
         assert got == loop(n) and all(type(d) is str for d in got)
+
+
+def test_trading_dates_array_equals_numpy_formatting():
+    """The columnar path's dates (integer-formatted U10 code points) equal np.datetime_as_string
+    of the same business days, to 10^6 samples (year 5855) and past year 9999 (NumPy's own
+    formatting takes over)."""
+    for n in (0, 1, 4, 5, 6, 1000, 1_000_000, 2_700_000):
+        days = np.busday_offset("2022-01-03", np.arange(n), roll="forward")
+        got = G.trading_dates_array(n)
+        assert np.array_equal(got, np.datetime_as_string(days, unit="D")), n
+        assert got.size == n

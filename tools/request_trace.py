@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""The bench's timed requests out of a rocprofv3 kernel trace (rocprofv3 --kernel-trace
+--output-format csv of `python bench.py --no-cpu --no-calib --steps K --warmup W`).
+
+bench.py issues, on one stream and in this order, for the configured request shape:
+  1 correctness-check request (device path), 1 host-API request (the same kernels), W warm-up
+  requests, K timed requests, then host-API and HIP-event-timed requests.
+Every one of them is a request-shaped dispatch (the same kernel(s) and grid).  This script picks
+the request-shaped dispatches (the most frequent (kernel, grid) of the COS kernels), takes the
+K timed ones (positions W + 2 .. W + K + 1 among the requests; a request of several kernels is
+counted once per its first kernel) and reports their mean / median device duration and the wall
+span of the timed window per request -- the number comparable to bench.py's ms_per_step.
+
+usage: python tools/request_trace.py TRACE.csv --steps K --warmup W [--out JSON]
+"""
+import argparse
+import collections
+import csv
+import json
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--warmup", type=int, required=True)
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    rows = []
+    with open(a.trace) as fh:
+        for r in csv.DictReader(fh):
+            if "cos_" not in r["Kernel_Name"] and "table_prologue" not in r["Kernel_Name"]:
+                continue
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"].split("(")[0],
+                         int(r["Grid_Size_X"]), int(r["Start_Timestamp"]),
+                         int(r["End_Timestamp"])))
+    rows.sort()
+    shape = collections.Counter((k, g) for _, k, g, _, _ in rows).most_common()
+    # a request = one dispatch of each kernel of the dominant shape(s) with the same count
+    top = shape[0][1]
+    kinds = [s for s, c in shape if c == top]
+    first = kinds[0]
+    reqs, cur = [], None
+    for d, k, g, s, e in rows:
+        if (k, g) not in kinds:
+            continue
+        if (k, g) == first:
+            cur = [s, e, e - s]
+            reqs.append(cur)
+        elif cur is not None:
+            cur[1] = e
+            cur[2] += e - s
+    lo, hi = a.warmup + 2, a.warmup + 2 + a.steps
+    timed = reqs[lo:hi]
+    durs = [t[2] / 1e3 for t in timed]          # device time of the request's kernels, us
+    span = (timed[-1][1] - timed[0][0]) / 1e3 / len(timed)
+    out = {"kernels": [f"{k} grid {g}" for k, g in kinds], "requests_in_trace": len(reqs),
+           "timed_requests": len(timed), "timed_positions": [lo, hi],
+           "device_us_mean": statistics.mean(durs), "device_us_median": statistics.median(durs),
+           "device_us_min": min(durs), "device_us_max": max(durs),
+           "wall_span_us_per_request": span,
+           "all_requests_device_us_mean": statistics.mean(t[2] / 1e3 for t in reqs)}
+    print(json.dumps(out, indent=1))
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

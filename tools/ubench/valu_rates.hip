@@ -24,6 +24,7 @@ __global__ __launch_bounds__(256) void k(double* out, double sx) {
     float f0 = x, f1 = f0 + 1, f2 = f0 + 2, f3 = f0 + 3, f4 = f0 + 4, f5 = f0 + 5, f6 = f0 + 6, f7 = f0 + 7;
     int i0 = threadIdx.x, i1 = i0 + 1, i2 = i0 + 2, i3 = i0 + 3, i4 = i0 + 4, i5 = i0 + 5,
         i6 = i0 + 6, i7 = i0 + 7;
+    double b0 = y, b1 = y + 1, b2 = y + 2, b3 = y + 3, b4 = y + 4, b5 = y + 5, b6 = y + 6, b7 = y + 7;
     d4 c0 = {x, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
     for (int it = 0; it < kIter; ++it) {
         if constexpr (kind == 0) {
@@ -55,6 +56,11 @@ __global__ __launch_bounds__(256) void k(double* out, double sx) {
 #define S(j) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(f##j) : "v"((float)x), "v"((float)y));
             REP8(S)
 #undef S
+        } else if constexpr (kind == 8) {     // 16 chains: two independent FMAs per accumulator
+#define S(j) asm volatile("v_fma_f64 %0, %2, %3, %0\n\tv_fma_f64 %1, %3, %2, %1" \
+                          : "+v"(a##j), "+v"(b##j) : "v"(x), "v"(y));
+            REP8(S)
+#undef S
         } else {
             c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c0, 0, 0, 0);
             c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y, x, c1, 0, 0, 0);
@@ -64,11 +70,12 @@ __global__ __launch_bounds__(256) void k(double* out, double sx) {
     }
     out[blockIdx.x * 256 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + f0 + f1 + f2 +
                                           f3 + f4 + f5 + f6 + f7 + i1 + i2 + i3 + i4 + i5 + i6 +
-                                          i7 + c0.x + c1.y + c2.z + c3.w;
+                                          i7 + c0.x + c1.y + c2.z + c3.w + b0 + b1 + b2 + b3 +
+                                          b4 + b5 + b6 + b7;
 }
 
 template <int kind>
-void run(const char* name, int n_inst_per_iter, double* out, int blocks) {
+void run(const char* name, int n_inst_per_iter, double* out, int blocks = 1024) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
@@ -81,14 +88,14 @@ void run(const char* name, int n_inst_per_iter, double* out, int blocks) {
     (void)hipEventElapsedTime(&ms, e0, e1);
     // wave-instructions per SIMD: blocks * 4 waves * kIter * n / 1024 SIMDs
     const double wi = (double)blocks * 4 * kIter * n_inst_per_iter / 1024.0;
-    printf("%-8s %8.3f ms  %6.2f ns per wave-instruction per SIMD  (= %5.2f cycles at 2.4 GHz)\n",
-           name, ms, ms * 1e6 / wi, ms * 1e6 / wi * 2.4);
+    printf("%-8s %5d blocks %8.3f ms  %6.2f ns per wave-instruction per SIMD  (= %5.2f cycles "
+           "at 2.4 GHz)\n", name, blocks, ms, ms * 1e6 / wi, ms * 1e6 / wi * 2.4);
 }
 
 int main() {
     double* out;
     const int blocks = 1024;   // 256 CUs x 4 blocks of 4 waves: 4 waves per SIMD
-    (void)hipMalloc(&out, (size_t)blocks * 256 * 8);
+    (void)hipMalloc(&out, (size_t)4096 * 256 * 8);
     run<0>("fma_vvv", 8, out, blocks);
     run<1>("fma_vsv", 8, out, blocks);
     run<2>("mul", 8, out, blocks);
@@ -97,6 +104,11 @@ int main() {
     run<5>("int", 8, out, blocks);
     run<6>("fma_f32", 8, out, blocks);
     run<7>("mfma", 4, out, blocks);
+    run<8>("fma16", 16, out, blocks);
+    run<0>("fma_vvv", 8, out, 2048);       // 8 waves per SIMD
+    run<8>("fma16", 16, out, 2048);
+    run<0>("fma_vvv", 8, out, 256);        // 1 wave per SIMD
+    run<8>("fma16", 16, out, 256);
     (void)hipFree(out);
     return 0;
 }
