@@ -51,6 +51,38 @@ def cf_complex_golden():
 
 
 @pytest.fixture(scope="session")
+def calib_noise():
+    with open(os.path.join(GOLDEN, "calib_noise.json")) as fh:
+        return json.load(fh)
+
+
+def assert_in_noise_ensemble(res, runs, ens, reference_starts, label):
+    """calibrate(300, 3) on the reference's test market (np.random.seed(0) starts) against the
+    reference algorithm's outcomes under last-bit price noise (tests/golden/calib_noise.json,
+    member 0 = the reference's own run): the winner CONVERGED inside the ensemble's band of
+    final losses (x/ 2 slack: 12 members sample a chaotic map), start 0 exactly as every member
+    (nit 0, 'ABNORMAL: ', the Feller kink), starts 1 and 2 with a message some member ends with
+    and a loss inside the members' range for that start.  Prints per-start (nit, message, fun)
+    beside the reference's."""
+    import numpy as np
+    lo, hi = ens["final_loss_min"] / 2, ens["final_loss_max"] * 2
+    assert res.message.startswith("CONVERGENCE") and res.success, (label, res.message)
+    assert lo <= res.final_loss <= hi, (label, res.final_loss, lo, hi)
+    for s, ((r, _), ref) in enumerate(zip(runs, reference_starts)):
+        members = [m["starts"][s] for m in ens["members"]]
+        print(f"{label} start {s}: nit {r.nit:3d} {r.message!r:58} fun {r.fun:.6e}   reference: "
+              f"nit {ref['nit']:3d} {ref['message']!r:58} fun {ref['fun']:.6e}")
+        assert r.message in {m["message"] for m in members}, (label, s, r.message)
+        if s == 0:
+            assert r.nit == 0 and r.message == "ABNORMAL: "
+        f_lo = min(m["fun"] for m in members) / 2
+        f_hi = max(m["fun"] for m in members) * 2
+        assert f_lo <= r.fun <= f_hi, (label, s, r.fun, f_lo, f_hi)
+    assert res.final_loss == min(r.fun for r, _ in runs)
+    assert np.isfinite(res.final_loss)
+
+
+@pytest.fixture(scope="session")
 def grid():
     with np.load(os.path.join(GOLDEN, "pricing_grid.npz")) as z:   # allow_pickle=False default
         return {k: z[k] for k in z.files}

@@ -56,12 +56,18 @@ def test_device_driver_robust_start(dh, calib_golden):
     assert not res.success
 
 
-def test_device_driver_calibrate_seed0(dh, calib_golden):
+def test_device_driver_calibrate_seed0(dh, calib_golden, calib_noise):
+    """As test_gpu_parity.test_calibrate_seed0, on the device-resident L-BFGS-B: the winner and
+    every start inside the reference algorithm's noise ensemble (tests/golden/calib_noise.json)."""
+    from conftest import assert_in_noise_ensemble
+    from dhcos.calibrator import run_starts_device
     np.random.seed(0)
     cal = _cal(dh, calib_golden)
     r = cal.calibrate(maxiter=300, multi_start=3, driver="device")
-    assert r.success and r.message.startswith("CONVERGENCE")
-    assert r.final_loss < 1e-6
+    x0s = [np.array(s["x0"]) for s in calib_golden["calibrate_seed0_starts"]]
+    runs = run_starts_device(_cal(dh, calib_golden), x0s, 300)
+    assert_in_noise_ensemble(r, runs, calib_noise, calib_golden["calibrate_seed0_starts"],
+                             "device")
     assert rel_close(r.model_prices, cal.market_prices, 5e-3, 0).all()
     assert 0 < r.calibration_time < 5.0
     assert cal.lockstep_launches > 0

@@ -328,20 +328,24 @@ def test_reference_test_4_1_direct_minimize(dh, calib_golden):
     assert cal.n_calls == g["n_calls"]
 
 
-def test_calibrate_seed0(dh, calib_golden):
+def test_calibrate_seed0(dh, calib_golden, calib_noise):
     """calibrate(300, 3) under np.random.seed(0).
 
     Trajectory parity is not a well-posed target here: the FD gradient divides ~1e-14 loss noise
     by h = 1e-8, and the reference's own starts 1/2 change outcome under 1e-15 relative price
-    noise (tests/test_calibration_sensitivity.py).  Asserted instead: the robust start (0, the
-    Feller-kink start, Q12) reproduces the reference exactly, and the winner is a converged fit at
-    least as good as the band the reference's own noise ensemble spans."""
+    noise (tests/test_calibration_sensitivity.py).  Asserted instead, per start and for the
+    winner, membership in the reference algorithm's own noise ensemble
+    (tests/golden/calib_noise.json: 12 runs, member 0 the reference's 1.0197e-7 / nit 33;
+    winners 3.5e-8 .. 8.0e-7, all CONVERGENCE), start 0 exactly as the reference."""
+    from conftest import assert_in_noise_ensemble
+    from dhcos.calibrator import run_starts
     g = calib_golden
     np.random.seed(0)
     cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
     r = cal.calibrate(maxiter=300, multi_start=3)
-    assert r.success and r.message.startswith("CONVERGENCE")
-    assert r.final_loss < 1e-6                  # reference: 1.0197e-7; noise band 6.5e-8..8e-7
+    x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
+    runs = run_starts(dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"]), x0s, 300)
+    assert_in_noise_ensemble(r, runs, calib_noise, g["calibrate_seed0_starts"], "scipy")
     assert rel_close(r.model_prices, cal.market_prices, 5e-3, 0).all()
     assert r.calibration_time is not None and r.calibration_time < g["calibrate_seed0"]["seconds"]
 
