@@ -186,6 +186,8 @@ def kernel_label(ctx):
     """Kernels of the last request on ctx (after the bench's own launches)."""
     if ctx.last_path == _native.PATH_FUSED:
         return "cos_fused_kernel (after table_prologue_kernel on grids of >= 8,192 tables)"
+    if ctx.last_path == _native.PATH_GEN:
+        return "cos_gen_kernel (fused small-tile generator kernel, one launch per batch)"
     return "cos_table_kernel + cos_option[_small]_kernel"
 
 
@@ -365,11 +367,14 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
     flop = P * G * N * FLOP_TAB + P * M * (N - 1) * FLOP_TERM + P * M * FLOP_OPT
     survey_flop = P * G * N * 716 + P * M * N * 120
     alg_bytes = P * 16 * 8 + M * 17 + P * M * 8
-    # launch pairs per batch: the library chunks param sets so one chunk's tables stay within
-    # 256 MiB (dh_kernels.hip launch_price: per set = groups x (N + 8 consts + clamp words +
-    # largest group) doubles); the committed PMC bytes are per launch pair
+    # launches per batch: the split path (--path split) chunks param sets so one chunk's tables
+    # stay within 256 MiB (dh_kernels.hip launch_price: per set = groups x (N + 8 consts + clamp
+    # words + largest group) doubles), the committed PMC bytes being per launch pair; the
+    # default generator kernel (cos_gen_kernel) is one launch
     per_p = G * (N + 8 + 1 + 8) * 8
     n_chunks = -(-P // max(1, (256 << 20) // per_p))
+    if surf.ctx.last_path == _native.PATH_GEN:      # one fused launch for the whole batch
+        n_chunks = 1
     tr = pmc_traffic(args.config)
     roofline = make_roofline(flop, survey_flop, ker_ms,
                              pmc_executed(args.config, ker_ms, n_chunks),

@@ -74,9 +74,12 @@ int dh_ctx_set_exact(dh_ctx* ctx, int on);
  * grids: a COS-table launch then the lane-per-option-group kernel); otherwise the table launch
  * then an option launch.  FUSED / SPLIT force one of the two where it applies.  Both produce
  * the same bits; the choice only changes speed.                                              */
-enum { DH_PATH_AUTO = 0, DH_PATH_SPLIT = 1, DH_PATH_FUSED = 2 };
+enum { DH_PATH_AUTO = 0, DH_PATH_SPLIT = 1, DH_PATH_FUSED = 2, DH_PATH_GEN = 3 };
 int dh_ctx_set_path(dh_ctx* ctx, int path);
-/* DH_PATH_FUSED or DH_PATH_SPLIT: the kernels the last fast-path request ran (0 before any). */
+/* DH_PATH_FUSED, DH_PATH_SPLIT or DH_PATH_GEN (AUTO only: generator grids -- every maturity group
+ * one tile of <= 16 options in a call of >= 65,536 tasks -- priced by one fused small-tile
+ * launch, agreeing with the other paths to ~1e-15): the kernels the last fast-path request ran
+ * (0 before any).                                                                              */
 int dh_ctx_last_path(dh_ctx* ctx);
 /* Diagnostics (only in the DH_STAMPS build, `make stamps`; the production library returns
  * DH_E_ARG): record per-block s_memtime phase stamps of the COS kernels, read the last request's. */

@@ -1280,6 +1280,244 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A_, 
 }
 
 // ----------------------------------------------------------------------------------------------
+// fused small-tile kernel (generator grids: every maturity group one tile of <= kSmallTile
+// options, >= kSmallMinTasks tasks): a persistent block takes TB tables at a time, forms their
+// expanded tables (T2_k, T6_k) in LDS -- no table round trip through L2/MALL and no second
+// launch -- then prices their options on lanes (table, option, k-block):
+//   * prologue: one lane per table (table_prologue, the split path's constants);
+//   * CF: TPT = 256 / TB threads per table, entries k = t, t + TPT, ... (cf_phase_re), each
+//     stored as (T2, T6) with the table kernel's expressions; c0 / c5 / w0 summed per thread in
+//     increasing k, then a TPT-lane butterfly;
+//   * options: OP (a power of two >= the largest tile) option slots per table x S = TPT / OP
+//     k-blocks per option: lane j of an option sums k in [1 + j L, 1 + (j + 1) L), L = ceil((N - 1)
+//     / S), cos/sin(k th) by the step-th Chebyshev recurrence re-anchored by an exact sincos every
+//     kAnchor terms, then an S-lane butterfly; clamp-widened options (double_heston.py:135-137)
+//     are priced afterwards by the whole wave (clamped_term_sum, lanes over k);
+//   * loss: per table the options' rel^2 / invalid flags summed in option order, then the
+//     fence-free hand-off of the other request kernels (one task = one (p, tile)).
+// Prices agree with the split / fused paths to ~1e-15 relative (another summation order), as the
+// lane-per-option-group small-tile kernel's did.
+// ----------------------------------------------------------------------------------------------
+template <int TB>
+__global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP) {
+    const PriceArgs& A = karg_ref<PriceArgs, 0>();   // read in place (karg_ref)
+    if (halted(A)) return;
+    constexpr int TPT = kBlock / TB;                 // threads per table (CF), <= 64
+    static_assert(TPT <= 64 && TPT >= kSmallTile, "one table's lanes inside one wave");
+    extern __shared__ __attribute__((aligned(16))) double2 gtab[];   // [TB][N] (T2, T6)
+    __shared__ double shc[TB][kTabC];
+    __shared__ double ks[TB][3];                     // c0, c5, w0
+    __shared__ double osse[TB][kSmallTile], obad[TB][kSmallTile];
+    __shared__ double2 sct[dh::kMathTab];
+    dh::load_math_tables(sct, 0);                    // synchronised by the first barrier
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int N = A.N;
+    const int tpp = tabs_per_p(A);
+    const int64_t n_q = A.np * tpp;
+    const int S = TPT / OP;                          // k-blocks per option
+    const int Lk = (N - 1 + S - 1) / S;              // terms per k-block
+    const int it = t / TPT, sub = t % TPT;           // CF phase: table slot, thread in table
+    const int io = t / TPT, oo = (t % TPT) / S, jj = t % S;   // option phase: table, option, k-block
+    for (int64_t b0 = (int64_t)blockIdx.x * TB; b0 < n_q; b0 += (int64_t)gridDim.x * TB) {
+        const int nb = (int)min<int64_t>(TB, n_q - b0);
+        if (t < nb) table_prologue(A, b0 + t, shc[t]);
+        __syncthreads();
+        // ---- CF entries of table slot `it` into LDS ----
+        if (it < nb) {
+            const double* c = shc[it];
+            const double a = c[0], eb = c[2], ea = c[3], scale = c[4], piba = c[5];
+            const double S0 = c[22], T = c[24];
+            dh::CfConsts CC;
+            {
+                double* cc = (double*)&CC;
+                for (int j = 0; j < 16; ++j) cc[j] = c[6 + j];
+            }
+            double2* tb = gtab + (size_t)it * N;
+            double c0 = 0.0, c5 = 0.0, w0 = 0.0;
+            table_entries<TPT>(CC, sub, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
+                if (k == 0) {
+                    w0 = 0.5 * w;
+                    tb[0] = make_double2(0.0, 0.0);
+                    return;
+                }
+                const double T2 = w * S0 * dh::drcp(1.0 + u * u);
+                tb[k] = make_double2(T2, -(T2 * dh::drcp(u)));
+                const double cb = (k & 1) ? -1.0 : 1.0;
+                c0 += T2 * eb * cb;
+                c5 += T2 * ea;
+            });
+            c0 = xor_sum(c0, TPT);
+            c5 = xor_sum(c5, TPT);
+            w0 = xor_sum(w0, TPT);                   // one nonzero term (thread 0's)
+            if (sub == 0) {
+                ks[it][0] = c0;
+                ks[it][1] = c5;
+                ks[it][2] = w0;
+            }
+        }
+        __syncthreads();
+        // ---- options of table slot `io`: option oo, k-block jj ----
+        const int64_t q = b0 + io;
+        const bool tab_ok = io < nb;
+        const double* c = shc[tab_ok ? io : 0];
+        const double a = c[0], b = c[1], piba = c[5], S0 = c[22];
+        const int g0 = (int)c[27], gn = tab_ok ? (int)c[28] : 0;
+        const bool in = tab_ok && oo < gn;
+        const int m = g0 + (in ? oo : 0);
+        double K = 0.0, xK = 0.0, ratio = 1.0;
+        if (in) {
+            K = option_strike(A, m, S0);
+            xK = option_logk(K, S0, ratio);
+        }
+        const bool cl = in && (xK - 0.1 < a || xK + 0.1 > b);
+        const bool use = in && !cl;
+        double sum = 0.0;
+        {
+            const double th = use ? piba * (xK - a) : 0.0;
+            double st, ct;
+            dh::dsincos_t(th, sct, &st, &ct);
+            const double c2 = 2.0 * ct;
+            const double2* tb = gtab + (size_t)(tab_ok ? io : 0) * N;
+            const int k_lo = 1 + jj * Lk, k_hi = min(N, k_lo + Lk);
+            double sc = 0.0, ss = 0.0;
+            for (int k0 = k_lo; k0 < k_hi; k0 += kAnchor) {
+                double cx, sx;                                     // cos / sin (k0 th)
+                if (k0 == 1) {
+                    cx = ct;
+                    sx = st;
+                } else {
+                    dh::dsincos_t((double)k0 * piba * (xK - a), sct, &sx, &cx);
+                }
+                double cp = cx * ct + sx * st;                     // cos / sin ((k0 - 1) th)
+                double sp = sx * ct - cx * st;
+                // four steps per iteration with the entries read four ahead (immediate LDS
+                // offsets), x_k / x_{k-1} swapping registers (angle_sum_1 with G = 1)
+                const int kend = min(k_hi, k0 + kAnchor);
+                int k = k0;
+                const double2* tq = tb + k;
+                double2 t0 = tq[0], t1 = tq[1], t2 = tq[2], t3 = tq[3];
+                for (; k + 3 < kend; k += 4) {
+                    tq += 4;
+                    const double2 n0 = tq[0], n1 = tq[1], n2 = tq[2], n3 = tq[3];
+                    sc = fma(t0.x, cx, sc);
+                    ss = fma(t0.y, sx, ss);
+                    cp = fma(c2, cx, -cp);                         // x_{k+1} into (cp, sp)
+                    sp = fma(c2, sx, -sp);
+                    sc = fma(t1.x, cp, sc);
+                    ss = fma(t1.y, sp, ss);
+                    cx = fma(c2, cp, -cx);                         // x_{k+2} into (cx, sx)
+                    sx = fma(c2, sp, -sx);
+                    sc = fma(t2.x, cx, sc);
+                    ss = fma(t2.y, sx, ss);
+                    cp = fma(c2, cx, -cp);
+                    sp = fma(c2, sx, -sp);
+                    sc = fma(t3.x, cp, sc);
+                    ss = fma(t3.y, sp, ss);
+                    cx = fma(c2, cp, -cx);
+                    sx = fma(c2, sp, -sx);
+                    t0 = n0;
+                    t1 = n1;
+                    t2 = n2;
+                    t3 = n3;
+                }
+                for (; k < kend; ++k) {                            // the last < 4 steps
+                    sc = fma(t0.x, cx, sc);
+                    ss = fma(t0.y, sx, ss);
+                    const double nc = fma(c2, cx, -cp), ns = fma(c2, sx, -sp);
+                    cp = cx;
+                    sp = sx;
+                    cx = nc;
+                    sx = ns;
+                    t0 = t1;
+                    t1 = t2;
+                    t2 = t3;
+                }
+            }
+            sum = use ? sc + ss : 0.0;
+        }
+        sum = xor_sum(sum, S);
+        const int64_t p = A.p0 + (tab_ok ? q / tpp : 0);
+        if (use && jj == 0) {
+            const Consts C{ks[io][0], 0.0, ks[io][1], ks[io][2], a, b, c[2], c[3]};
+            const double price = c[29] * option_sum(C, A.call[m] != 0, S0, K, xK, ratio, sum);
+            if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
+            if (A.part_sse) {
+                const double mk = A.mkt[m];
+                const double rel = (price - mk) / mk;
+                osse[io][oo] = rel * rel;
+                obad[io][oo] = (isnan(price) || isinf(price) || price <= 0.0) ? 1.0 : 0.0;
+            }
+        }
+        // ---- clamp-widened options: the whole wave prices each (lanes over k) ----
+        unsigned long long mask = __ballot(cl && jj == 0);
+        while (mask) {
+            const int l = __ffsll((long long)mask) - 1;
+            mask &= mask - 1;
+            const int src = (t & ~63) + l;                         // the clamped option's lane
+            const int li = src / TPT, lo_ = (src % TPT) / S;
+            const double* cl_c = shc[li];
+            const double x = __shfl(xK, l, 64), Kl = __shfl(K, l, 64);
+            const int ml = (int)cl_c[27] + lo_;
+            const int64_t pl = A.p0 + (b0 + li) / tpp;
+            const Params P = dh::load_params(A.prm + pl * DH_PARAM_STRIDE);
+            const double ac = (x - 0.1 < cl_c[0]) ? x - 0.1 : cl_c[0];      // Python min/max
+            const double bc = (x + 0.1 > cl_c[1]) ? x + 0.1 : cl_c[1];
+            double v = clamped_term_sum(P, cl_c[24], Kl, x, ac, bc, A.call[ml] != 0, lane, 64, N,
+                                        sct);
+            v = xor_sum(v, 64);
+            if (lane == 0) {
+                const double price = cl_c[29] * v;
+                if (A.out) A.out[pl * A.out_stride + A.perm[ml]] = price;
+                if (A.part_sse) {
+                    const double mk = A.mkt[ml];
+                    const double rel = (price - mk) / mk;
+                    osse[li][lo_] = rel * rel;
+                    obad[li][lo_] = (isnan(price) || isinf(price) || price <= 0.0) ? 1.0 : 0.0;
+                }
+            }
+        }
+        if (A.part_sse) {
+            __syncthreads();
+            // one lane per table: the options' terms in option order, then the hand-off
+            if (t < nb) {
+                const double* cc = shc[t];
+                const int ng = (int)cc[28];
+                double acc = 0.0;
+                int nbad = 0;
+                for (int o = 0; o < ng; ++o) {
+                    acc += osse[t][o];
+                    nbad += obad[t][o] != 0.0 ? 1 : 0;
+                }
+                const int64_t qq = b0 + t;
+                const int64_t pp = A.p0 + qq / tpp;
+                const int tile = A.paired ? 0 : (int)(qq % tpp);
+                const int64_t task = A.paired ? pp : pp * A.n_tiles + tile;
+                __hip_atomic_store(&A.part_sse[task], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&A.part_bad[task], nbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned old = __hip_atomic_fetch_add(&A.counter[pp * kCounterStride], 1u,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int ntask = A.paired ? 1 : A.n_tiles;
+                if (old == (unsigned)ntask - 1u) {
+                    const int64_t base_i = A.paired ? pp : pp * A.n_tiles;
+                    double s2 = 0.0;
+                    int bad = 0;
+                    for (int j = 0; j < ntask; ++j) {                // tile order
+                        s2 += __hip_atomic_load(&A.part_sse[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        bad += __hip_atomic_load(&A.part_bad[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    A.sse[pp] = s2;
+                    A.n_bad[pp] = bad;
+                    __hip_atomic_store(&A.counter[pp * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        __syncthreads();                                 // gtab / shc / osse reused
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // fused request kernel: one block per table (p, g) whose maturity group is one tile.
 //   prologue (thread 0) || option staging (other waves first) -> CF loop writing the expanded
 //   table straight into LDS + k-sums -> clamp scan -> fixed-order constants || rotations ->
@@ -1689,9 +1927,14 @@ struct HostBuf {
 // with few tables per slot, e.g. C3: 4,200 tables on 3,072 one-wave slots).
 struct dh_ctx_view {
     int resident[3] = {0, 0, 0};
+    int resident_gen[3] = {0, 0, 0};   // cos_gen_kernel<16 / 8 / 4> at its N's LDS
 };
 
 int fused_tpt(int N) { return N <= 64 ? 64 : (N <= 128 ? 128 : 256); }
+
+// cos_gen_kernel<TB>: TB tables' (T2, T6) in LDS, <= 32 KB per block (three blocks per CU)
+constexpr int gen_max_n(int TB) { return 2048 / TB; }
+int gen_tb(int N) { return N <= gen_max_n(16) ? 16 : (N <= gen_max_n(8) ? 8 : (N <= gen_max_n(4) ? 4 : 0)); }
 
 int table_tpt(const dh_ctx_view& v, int64_t n_q, int N) {
     auto cost = [&](int i) {
@@ -1852,6 +2095,14 @@ int ensure_attrs(dh_ctx* ctx) {
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fns[i], kBlock, lds));
         ctx->view.resident[i] = std::max(1, per_cu) * std::max(1, cus);
     }
+    const void* gens[3] = {(const void*)cos_gen_kernel<16>, (const void*)cos_gen_kernel<8>,
+                           (const void*)cos_gen_kernel<4>};
+    for (int i = 0; i < 3; ++i) {               // LDS of the largest N each build takes
+        const size_t lds = (size_t)gen_max_n(16 >> i) * (16 >> i) * sizeof(double2);
+        int per_cu = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gens[i], kBlock, lds));
+        ctx->view.resident_gen[i] = std::max(1, per_cu) * std::max(1, cus);
+    }
     ctx->attr_set = true;
     return DH_OK;
 }
@@ -1955,6 +2206,31 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     return DH_OK;
 }
 
+// The generator batch path: every maturity group one tile of <= kSmallTile options, a large call
+// (DESIGN.md 3.3): one persistent cos_gen_kernel launch for the whole request.
+int launch_gen(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st, int TB) {
+    const int tpp = A0.paired ? 1 : A0.n_groups;
+    const int max_nopt = A0.paired ? 1 : A0.opt_cap;
+    int OP = 1;
+    while (OP < max_nopt) OP *= 2;
+    PriceArgs A = A0;
+    A.p0 = 0;
+    A.np = A0.P;
+    A.partials_only = 0;
+    const int64_t n_q = A.np * tpp;
+    const int gi = TB == 16 ? 0 : (TB == 8 ? 1 : 2);
+    const int64_t blocks = std::min<int64_t>((n_q + TB - 1) / TB, ctx->view.resident_gen[gi]);
+    const size_t lds = (size_t)TB * A.N * sizeof(double2);
+    if (blocks <= 0 || OP > kBlock / TB) return fail(DH_E_ARG, "generator kernel shape");
+    switch (TB) {
+        case 16: hipLaunchKernelGGL((cos_gen_kernel<16>), dim3((unsigned)blocks), dim3(kBlock), lds, st, A, OP); break;
+        case 8: hipLaunchKernelGGL((cos_gen_kernel<8>), dim3((unsigned)blocks), dim3(kBlock), lds, st, A, OP); break;
+        default: hipLaunchKernelGGL((cos_gen_kernel<4>), dim3((unsigned)blocks), dim3(kBlock), lds, st, A, OP); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return DH_OK;
+}
+
 // Table kernel then option kernel per chunk of param sets; the chunk keeps the table workspace
 // within kTableBudget (L2/MALL-resident between the two launches).  Requests whose maturity
 // groups are single tiles may instead run as one fused launch (ctx->path).
@@ -1977,6 +2253,14 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
                                        (ctx->path == DH_PATH_AUTO && !small_call));
         ctx->last_path = fused ? DH_PATH_FUSED : DH_PATH_SPLIT;
         if (fused) return launch_fused(ctx, A0, st);
+        // generator grids: one fused small-tile launch (PATH_SPLIT keeps the table + option
+        // kernels, for A/B)
+        const int tb = gen_tb(N);
+        if (small_call && ctx->path == DH_PATH_AUTO && tb &&
+            (A0.paired || A0.n_tiles == A0.n_groups)) {
+            ctx->last_path = DH_PATH_GEN;
+            return launch_gen(ctx, A0, st, tb);
+        }
     }
     const int tpp = A0.paired ? 1 : A0.n_groups;
     const int words = cl_words(A0);

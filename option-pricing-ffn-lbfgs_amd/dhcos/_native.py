@@ -26,7 +26,7 @@ MAX_N = 2048                   # longest series of the table (fast) path (DH_MAX
 MAX_N_PER_TERM = 65536         # longest accepted; longer than MAX_N runs the per-term path
 STRIKE_ABSOLUTE = 0
 STRIKE_PCT_SPOT = 1
-PATH_AUTO, PATH_SPLIT, PATH_FUSED = 0, 1, 2
+PATH_AUTO, PATH_SPLIT, PATH_FUSED, PATH_GEN = 0, 1, 2, 3   # PATH_GEN: reported only (AUTO)
 STAMPS_PER_BLOCK = 24          # kStamps of the DH_STAMPS build (csrc/dh_kernels.hip)
 
 _dp = C.POINTER(C.c_double)
@@ -198,7 +198,8 @@ class Context:
 
     @property
     def last_path(self) -> int:
-        """PATH_FUSED or PATH_SPLIT: the kernels of the last fast-path request (0 before any)."""
+        """PATH_FUSED, PATH_SPLIT or PATH_GEN: the kernels of the last fast-path request (0
+        before any)."""
         return int(load().dh_ctx_last_path(self._h))
 
     def debug_stamps(self, on: bool):
@@ -613,5 +614,6 @@ def default_context(device: int | None = None) -> Context:
 __all__ = ["gen_draw", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "MAX_N_PER_TERM",
            "STRIKE_ABSOLUTE",
-           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "LIB_PATH", "SIGNATURES",
+           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN", "LIB_PATH",
+           "SIGNATURES",
            "Comm", "comm_id", "best_start", "COMM_ID_BYTES"]

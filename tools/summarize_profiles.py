@@ -24,7 +24,7 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = ("cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel",
-           "table_prologue_kernel")
+           "table_prologue_kernel", "cos_gen_kernel")
 
 
 def short(name):
@@ -77,7 +77,9 @@ def main():
         # the request's kernels: the fused kernel if the config spends its time there, else the
         # table kernel + whichever option-kernel variant dominates (the others only serve the
         # bench's small spot-check calls)
-        if total.get("cos_fused_kernel", 0.0) >= max(total.values()):
+        if total.get("cos_gen_kernel", 0.0) >= max(total.values()):
+            req_kernels = ("cos_gen_kernel",)             # generator grids: one fused launch
+        elif total.get("cos_fused_kernel", 0.0) >= max(total.values()):
             # large fused grids run table_prologue_kernel ahead of the fused kernel
             pro = total.get("table_prologue_kernel", 0.0) >= 0.01 * total["cos_fused_kernel"]
             req_kernels = (("table_prologue_kernel",) if pro else ()) + ("cos_fused_kernel",)
