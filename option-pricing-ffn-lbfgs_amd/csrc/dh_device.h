@@ -304,11 +304,11 @@ __device__ __forceinline__ double datan2(double y, double x) {
 // ---- table-driven log, atan2 and exp of the CF loop --------------------------------------------
 // The CF's math tables in one LDS array of double2 (load_math_tables): [0, 128) sin / cos of
 // j pi/64 (dsincos_t), [128, 256) (invc, logc) of dlog_t, [256, 321) atan(j/64) (hi, lo) of
-// datan2_t, [321, 385) 2^(j/64) (hi, lo) of dexp_t.
+// datan2_t, [321, 353) 2^(j/64), j = 0..63, two per entry, of dexp_t.
 constexpr int kTabLog = 128;
 constexpr int kTabAtan = 256;
 constexpr int kTabExp = 321;
-constexpr int kMathTab = 385;
+constexpr int kMathTab = 353;
 
 // log(x) for normal x > 0 (glibc's table layout, tools/gen_logatan_tables.py): x = 2^k z with z
 // in [0.6875, 1.375) from the bits, subinterval i by the next 7 bits, r = z invc_i - 1 (one FMA,
@@ -367,24 +367,25 @@ __device__ __forceinline__ double datan2_t(double y, double x, const double2* __
     return copysign(a, y);
 }
 
-// exp(x) by a 64-entry table (glibc's layout, tools/gen_exp_table.py): x = (64 e + j) ln2/64 + r
-// with |r| <= ln2/128, q = 64 e + j rounded by the 1.5 * 2^52 shift (its low word IS q, so no
-// float-to-int conversion: a NaN x indexes a defined entry and stays NaN through r), e^r - 1 by
-// its Taylor series through r^5 (remainder < 4e-17 relative), then 2^e (hi + (hi (e^r - 1) + lo))
-// with 2^(j/64) = hi + lo.  ~1 ulp; 12 fp64 VALU against dexp's 19.  Finite x <= 709 (the CF's
-// exponents); callers select the overflow / underflow ends.
+// exp(x) by a 64-entry table (tools/gen_exp_table.py): x = (64 e + j) ln2/64 + r with |r| <=
+// ln2/128, q = 64 e + j rounded by the 1.5 * 2^52 shift (its low word IS q, so no float-to-int
+// conversion: a NaN x indexes a defined entry and stays NaN through r), e^r - 1 by its Taylor
+// series through r^5 (remainder < 4e-17 relative), then 2^e (t + t (e^r - 1)) with t = 2^(j/64)
+// correctly rounded.  ~1 ulp (a hi + lo table would give ~0.5 ulp but held two more VGPRs live
+// across the polynomial: spills in the <= 96-VGPR fused build); 11 fp64 VALU against dexp's 19.
+// Finite x <= 709 (the CF's exponents); callers select the overflow / underflow ends.
 __device__ __forceinline__ double dexp_t_core(double x, const double2* __restrict__ tab) {
     const double qd = fma(x, 0x1.71547652b82fep+6, kShift52);        // rint(x 64/ln2)
     const double q = qd - kShift52;
     const int qi = __double2loint(qd);                                // q as int32
     double r = fma(q, -0x1.62e42fefa39efp-7, x);                      // ln2/64, 2 parts
     r = fma(q, -0x1.abc9e3b39803fp-62, r);
-    const double2 t = tab[kTabExp + (qi & 63)];                       // 2^(j/64): hi, lo
     double p = fma(r, 0.008333333333333333, 0.041666666666666664);
     p = fma_k(r, p, 0.16666666666666666);
     p = fma_k(r, p, 0.5);
     const double em1 = fma(r * r, p, r);                              // e^r - 1
-    return ldexp(t.x + fma(t.x, em1, t.y), qi >> 6);
+    const double t = ((const double*)(tab + kTabExp))[qi & 63];       // 2^(j/64)
+    return ldexp(fma(t, em1, t), qi >> 6);
 }
 
 __device__ __forceinline__ double dexp_t(double x, const double2* __restrict__ tab) {

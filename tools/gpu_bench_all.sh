@@ -10,7 +10,7 @@ for c in ${CONFIGS:-c2 c1 c3 c4 c5}; do
 import json, sys
 d = json.load(open(sys.argv[1]))
 r = d["roofline"]; c = d.get("calibration", {})
-print(sys.argv[2], f"value {d['value']:.3e} {d['unit']}  step {d['ms_per_step']*1e3:.1f} us  frac {r['frac']}  exec {r.get('executed') and r['executed']['frac']}  "
+print(sys.argv[2], f"value {d['value']:.3e} {d['unit']}  step {d['ms_per_step']*1e3:.1f} us  frac {r['frac']}  basis {r.get('flop_basis', '')[:20]}  "
       f"cpu {d.get('cpu_baseline', {}).get('value', 0):.0f}/s x{d.get('cpu_baseline', {}).get('cores')}  calib {c.get('seconds', 0)*1e3:.1f} ms")
 PY
 done

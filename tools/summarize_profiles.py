@@ -52,9 +52,10 @@ def main():
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     md = [f"# Profile summary {args.tag}", "",
           "One request = cos_fused_kernel (every maturity group one tile: C1-C4; on grids of "
-          ">= 8,192 blocks, C4, preceded by table_prologue_kernel), or "
-          "cos_table_kernel + the option kernel (cos_option_kernel for multi-tile groups, "
-          "cos_option_small_kernel for large calls on <=16-option tiles: C5). Durations: "
+          ">= 8,192 blocks, C4, preceded by table_prologue_kernel), cos_gen_kernel (generator "
+          "grids, C5: one fused small-tile launch per batch), or cos_table_kernel + the option "
+          "kernel (--path split; cos_option_kernel for multi-tile groups, "
+          "cos_option_small_kernel for large calls on <=16-option tiles). Durations: "
           "rocprofv3 --kernel-trace --stats average; counters: per-launch medians of separate "
           "--pmc passes.", ""]
     for c in args.configs.split(","):
