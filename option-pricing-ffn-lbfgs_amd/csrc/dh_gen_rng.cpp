@@ -17,9 +17,15 @@
 // The caller passes NumPy's state (np.random.get_state()) in and sets the advanced state back,
 // so the global stream continues exactly where the reference's loop would leave it.  No FMA
 // contraction (the Makefile builds this file with -ffp-contract=off), libm log / sqrt as NumPy.
+#include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "dhcos.h"
 
@@ -84,7 +90,169 @@ struct LegacyRng {
         return f * x2;
     }
     double normal(double loc, double scale) { return loc + scale * next_gauss(); }
+
 };
+
+// The legacy doubles of an MT19937 stream a generation (624 words) at a time: the twist, the
+// tempering and the (a >> 5, b >> 6) conversion run as straight loops over the generation (the
+// compiler vectorises them) instead of a pos check per word.  While it runs, g.pos counts the
+// words READ; sync() sets it to the words a word-at-a-time consumer of the same doubles would
+// have taken, so the state handed back is the sequential loop's.
+struct DoubleStream {
+    LegacyRng& g;
+    uint32_t w[kMtN + 1];
+    double d[kMtN / 2 + 1];
+    int n = 0, i = 0;                // doubles in d, the next one
+    int s = 0, carry_in = 0;         // generation word d[] started at; d[0] took a carried word
+    int has_cw = 0;                  // a tempered word read but not yet paired
+    uint32_t cw = 0;
+    bool filled = false;
+    explicit DoubleStream(LegacyRng& g_) : g(g_) {}
+    double next() {
+        if (i == n) refill();
+        return d[i++];
+    }
+    void refill() {
+        do {
+            if (g.pos == kMtN) g.twist();
+            s = g.pos;
+            carry_in = has_cw;
+            int m = 0;
+            if (has_cw) w[m++] = cw;
+            const uint32_t* k = g.key + s;
+            const int len = kMtN - s;
+            for (int j = 0; j < len; ++j) {
+                uint32_t y = k[j];
+                y ^= (y >> 11);
+                y ^= (y << 7) & 0x9d2c5680u;
+                y ^= (y << 15) & 0xefc60000u;
+                y ^= (y >> 18);
+                w[m + j] = y;
+            }
+            m += len;
+            g.pos = kMtN;
+            n = m / 2;
+            for (int j = 0; j < n; ++j) {
+                const int32_t a = (int32_t)(w[2 * j] >> 5), b = (int32_t)(w[2 * j + 1] >> 6);
+                d[j] = (a * 67108864.0 + b) / 9007199254740992.0;
+            }
+            has_cw = m & 1;
+            if (has_cw) cw = w[m - 1];
+            i = 0;
+            filled = true;
+        } while (n == 0);
+    }
+    void sync() {
+        if (filled) g.pos = s + 2 * i - carry_in;
+    }
+    // The next k accepted polar pairs (next_gauss's do-while: x = 2 d - 1, rejected while
+    // r2 >= 1 or r2 == 0) into x1 / x2 / r2.  The candidates of up to 16 buffered pairs are
+    // tested together and the accepted ones taken by bit scan: no branch per rejection.
+    void pairs(int k, double* x1, double* x2, double* r2) {
+        int got = 0;
+        while (got < k) {
+            if (n - i < 2) {                        // a pair straddling a refill
+                const double a = 2.0 * next() - 1.0, b = 2.0 * next() - 1.0;
+                const double r = a * a + b * b;
+                if (r < 1.0 && r != 0.0) {
+                    x1[got] = a;
+                    x2[got] = b;
+                    r2[got] = r;
+                    ++got;
+                }
+                continue;
+            }
+            const int m = std::min((n - i) / 2, 16);
+            const double* q = d + i;
+            uint32_t mask = 0;
+            double ca[16], cb[16], cr[16];
+            for (int j = 0; j < m; ++j) {
+                ca[j] = 2.0 * q[2 * j] - 1.0;
+                cb[j] = 2.0 * q[2 * j + 1] - 1.0;
+                cr[j] = ca[j] * ca[j] + cb[j] * cb[j];
+                mask |= (uint32_t)(cr[j] < 1.0 && cr[j] != 0.0) << j;
+            }
+            int used = m;
+            while (mask) {
+                const int j = __builtin_ctz(mask);
+                mask &= mask - 1;
+                x1[got] = ca[j];
+                x2[got] = cb[j];
+                r2[got] = cr[j];
+                if (++got == k) {
+                    used = j + 1;
+                    break;
+                }
+            }
+            i += 2 * used;
+        }
+    }
+};
+
+// next_gauss's arithmetic after the pair: (f x2, f x1), f = sqrt(-2 log(r2) / r2)
+inline void pair_values(double x1, double x2, double r2, double& g_new, double& g_cached) {
+    const double f = std::sqrt(-2.0 * std::log(r2) / r2);
+    g_cached = f * x1;
+    g_new = f * x2;
+}
+
+// A fixed team of worker threads for one dh_gen_draw call: run(f) calls f(0..n-1) once each,
+// f(0) on the caller, and returns when all are done.
+class Team {
+  public:
+    explicit Team(int n) : n_(n) {
+        for (int w = 1; w < n_; ++w) th_.emplace_back([this, w] { loop(w); });
+    }
+    ~Team() {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return n_; }
+    void run(const std::function<void(int)>& f) {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            task_ = &f;
+            left_ = n_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> l(mu_);
+        done_.wait(l, [this] { return left_ == 0; });
+    }
+
+  private:
+    void loop(int w) {
+        int seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> l(mu_);
+            cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            const std::function<void(int)>* f = task_;
+            l.unlock();
+            (*f)(w);
+            l.lock();
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* task_ = nullptr;
+    int gen_ = 0, left_ = 0;
+    bool stop_ = false;
+};
+
+// Samples per chunk of the split draw (bounds its buffers), and below this many samples the
+// plain sequential loop
+constexpr int64_t kChunk = 1 << 16;
+constexpr int64_t kSplitMin = 4096;
 
 }  // namespace
 
@@ -106,17 +274,92 @@ extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss
     for (int j = 0; j < 13; ++j) range[j] = hi[j] - lo[j];
     const double beta = 1.0 - alpha;                      // (1 - alpha), :108
     double spot = spot0;
-    for (int64_t i = 0; i < n_samples; ++i) {
-        double* p = params + i * 13;
-        for (int j = 0; j < 13; ++j) p[j] = lo[j] + range[j] * g.next_double();   // :100-102
-        if (i > 0) {
-            const double* q = p - 13;
-            for (int j = 0; j < 13; ++j) p[j] = alpha * q[j] + beta * p[j];       // :105-109
-            spot = spot * (1.0 + g.normal(ret_mu, ret_sigma));                     // :112-116
+    if (n_samples < kSplitMin) {
+        for (int64_t i = 0; i < n_samples; ++i) {
+            double* p = params + i * 13;
+            for (int j = 0; j < 13; ++j) p[j] = lo[j] + range[j] * g.next_double();   // :100-102
+            if (i > 0) {
+                const double* q = p - 13;
+                for (int j = 0; j < 13; ++j) p[j] = alpha * q[j] + beta * p[j];       // :105-109
+                spot = spot * (1.0 + g.normal(ret_mu, ret_sigma));                     // :112-116
+            }
+            spots[i] = spot;
+            double* z = noise + i * n_opt;
+            for (int j = 0; j < n_opt; ++j) z[j] = g.normal(0.0, noise_sigma);        // :141
         }
-        spots[i] = spot;
-        double* z = noise + i * n_opt;
-        for (int j = 0; j < n_opt; ++j) z[j] = g.normal(0.0, noise_sigma);        // :141
+    } else {
+        // Large draws in three passes per chunk of samples, the same operations on the same
+        // values in the same order per value (so the same bits):
+        //   A (sequential): the MT19937 doubles (DoubleStream), the parameters and their AR(1)
+        //     blend, and for every gauss call either the accepted polar pair (x1, x2, r2) or a
+        //     reference to the pair whose cached half it returns, exactly as has_gauss toggles;
+        //   B (parallel over pairs): next_gauss's log / sqrt / products;
+        //   C (parallel over samples): the noise; then the spot walk (sequential).
+        const int64_t per = (int64_t)n_opt + 1;             // gauss calls per sample, at most
+        const int64_t cap = std::min(n_samples, kChunk) * per;
+        std::vector<double> px1(cap), px2(cap), pr2(cap), gn(cap), gc(cap);
+        // per sample: its first new pair in the chunk, and whether its first gauss call returns
+        // the value cached before it (the previous pair's f x1, or `pending` at pair -1)
+        std::vector<int32_t> first(kChunk);
+        std::vector<uint8_t> cached(kChunk);
+        double pending = g.gauss;                           // the value cached at entry
+        Team team((int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+        DoubleStream ds(g);
+        for (int64_t c0 = 0; c0 < n_samples; c0 += kChunk) {
+            const int64_t c1 = std::min(n_samples, c0 + kChunk);
+            int32_t np = 0;
+            int hg = g.has_gauss;
+            for (int64_t i = c0; i < c1; ++i) {             // A
+                double* p = params + i * 13;
+                for (int j = 0; j < 13; ++j) p[j] = lo[j] + range[j] * ds.next();   // :100-102
+                if (i > 0) {
+                    const double* q = p - 13;
+                    for (int j = 0; j < 13; ++j) p[j] = alpha * q[j] + beta * p[j]; // :105-109
+                }
+                // gauss calls: the spot return (i > 0, :112-116), then one per option (:141);
+                // the first takes the cached value if there is one, the rest run on new pairs,
+                // each serving two calls (f x2 now, f x1 cached for the next)
+                const int calls = n_opt + (i > 0 ? 1 : 0);
+                const int fresh = calls - hg;
+                first[i - c0] = np;
+                cached[i - c0] = (uint8_t)hg;
+                const int k = (fresh + 1) / 2;
+                ds.pairs(k, px1.data() + np, px2.data() + np, pr2.data() + np);
+                np += k;
+                hg = fresh > 0 ? (fresh & 1) : hg - calls;
+            }
+            g.has_gauss = hg;
+            const int nt = team.size();
+            team.run([&](int w) {                           // B
+                for (int64_t k = (int64_t)np * w / nt; k < (int64_t)np * (w + 1) / nt; ++k)
+                    pair_values(px1[k], px2[k], pr2[k], gn[k], gc[k]);
+            });
+            // gauss call c of sample i (chunk-relative r)
+            auto value = [&](int64_t r, int c) {
+                const int32_t f = first[r];
+                if (cached[r]) {
+                    if (c == 0) return f == 0 ? pending : gc[f - 1];
+                    --c;
+                }
+                return (c & 1) ? gc[f + c / 2] : gn[f + c / 2];
+            };
+            const int64_t ns = c1 - c0;
+            team.run([&](int w) {                           // C: noise
+                for (int64_t r = ns * w / nt; r < ns * (w + 1) / nt; ++r) {
+                    const int64_t i = c0 + r;
+                    const int c00 = i > 0 ? 1 : 0;
+                    double* z = noise + i * n_opt;
+                    for (int j = 0; j < n_opt; ++j) z[j] = 0.0 + noise_sigma * value(r, c00 + j);
+                }
+            });
+            for (int64_t i = c0; i < c1; ++i) {             // C: spots
+                if (i > 0) spot = spot * (1.0 + (ret_mu + ret_sigma * value(i - c0, 0)));
+                spots[i] = spot;
+            }
+            if (np > 0) pending = gc[np - 1];               // cached into the next chunk if
+        }                                                   // has_gauss is set
+        ds.sync();
+        g.gauss = g.has_gauss ? pending : 0.0;
     }
     std::memcpy(mt_key, g.key, sizeof(g.key));
     *mt_pos = g.pos;

@@ -9,7 +9,9 @@ import pytest
 from dhcos import generator as G
 
 
-@pytest.mark.parametrize("seed,n,pre", [(0, 3000, 0), (7, 1, 1), (123, 257, 3), (99, 0, 1)])
+# n >= 4096 takes the three-pass draw (dh_gen_rng.cpp), n > 65536 crosses one of its chunks
+@pytest.mark.parametrize("seed,n,pre", [(0, 3000, 0), (7, 1, 1), (123, 257, 3), (99, 0, 1),
+                                        (5, 4096, 0), (11, 66000, 1), (13, 5000, 2)])
 def test_native_draw_equals_numpy_loop(seed, n, pre):
     """pre = scalar normals drawn first, so the stream starts with / without a cached gauss."""
     np.random.seed(seed)
@@ -83,3 +85,21 @@ def test_trading_dates_array_equals_numpy_formatting():
         got = G.trading_dates_array(n)
         assert np.array_equal(got, np.datetime_as_string(days, unit="D")), n
         assert got.size == n
+
+
+@pytest.mark.parametrize("pos", [1, 311, 623, 624])
+def test_native_draw_any_stream_position(pos):
+    """The three-pass draw reads the MT19937 words a generation at a time and pairs them into
+    doubles; an odd entry position makes a double straddle a twist.  Same bits, same end state."""
+    np.random.seed(3)
+    st = list(np.random.get_state())
+    st[2] = pos
+    np.random.set_state(tuple(st))
+    want = G.draw_paths_numpy(4500)
+    after_want = np.random.get_state()
+    np.random.set_state(tuple(st))
+    got = G.draw_paths(4500)
+    after_got = np.random.get_state()
+    for a, b in zip(got, want):
+        assert np.array_equal(a, b)
+    assert np.array_equal(after_got[1], after_want[1]) and after_got[2:] == after_want[2:]
