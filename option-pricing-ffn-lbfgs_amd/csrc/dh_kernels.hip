@@ -418,6 +418,27 @@ __global__ __launch_bounds__(kBlock) void table_prologue_kernel(PriceArgs A, int
 #define DH_FUSED_WAVES_WIDE 5   // the one-option-per-lane-group variant for large grids (<= 96 VGPRs)
 #endif
 
+// Adaptive tail of the angle sums.  A table's terms k >= n_eff are not summed, n_eff - 1 being
+// the last k >= 1 with |T2_k| > tail_delta.  Past it |T6_k| = |T2_k| / u_k <= |T2_k| (b - a)/pi,
+// so the dropped part of S is at most (1 + (b - a)/pi) N delta = 2^-72 S0/(b - a), and a price
+// moves by at most e^{-rT} e^{xK} 2^-72 S0/(b - a) = e^{-rT} 2^-72 K/(b - a): below 2^-64 of its
+// own k = 0 term e^{-rT} w0 V0 (w0 = 1/(b - a); V0 >= 0.0048 K because the log-strike lies at
+// least 0.1 inside [a, b] -- clamp-widened options take the per-term path), i.e. far inside the
+// price's rounding.  The characteristic function decays like exp(-c u): at N = 512 (C3) a table
+// keeps ~26% of its terms, at N = 256 ~46%, at N = 128 ~97%.  Every path forms n_eff from the
+// same T2_k values with the same expressions, so fused and split keep their identical bits.
+// NaN / inf entries (and a NaN delta) always count as kept: a NaN still reaches the price.
+__device__ __forceinline__ double tail_delta(double S0, double ba, int N) {
+    return 0x1.0p-72 * S0 / (ba * (1.0 + ba * (1.0 / dh::kPi)) * (double)N);
+}
+__device__ __forceinline__ int tail_keep(int k, double T2, double delta) {
+    return fabs(T2) <= delta ? 0 : k + 1;
+}
+__device__ __forceinline__ int xor_max_i(int v, int width) {
+    for (int off = 1; off < width; off <<= 1) v = max(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
 // CF entries of one table slot (thread t of TPT): k = t, t + TPT, ..., emitted in increasing k
 // (the k-sums' order) as emit(k, u_k, w_k).
 template <int TPT, typename F>
@@ -479,7 +500,9 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             const double S0 = c[22], T = c[24], lo = c[25], hi = c[26];
             const int g0 = (int)c[27], gn = has ? (int)c[28] : 0;
             double* t2 = t2s + (TPT > 64 ? slot * N : 0);
-            double c0 = 0.0, c1 = 0.0, c5 = 0.0, w0 = 0.0;
+            double c0 = 0.0, c5 = 0.0, w0 = 0.0;
+            const double delta = tail_delta(S0, b - a, N);
+            int ne = 0;
             if (has) {
                 dh::CfConsts CC;
                 {
@@ -502,6 +525,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                     if (TPT == 64) {
                         c0 += T2 * eb * cb;
                         c5 += T2 * ea;
+                        ne = max(ne, tail_keep(k, T2, delta));
                     } else {
                         t2[k] = T2;
                     }
@@ -518,17 +542,19 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                         const double cb = (k & 1) ? -1.0 : 1.0;
                         c0 += T2 * eb * cb;
                         c5 += T2 * ea;
+                        ne = max(ne, tail_keep(k, T2, delta));
                     }
                 }
             }
             if (has && wv == 0) {
-                // c1 is a sum of zeros and w0 has one nonzero term (lane 0's): their butterflies
-                // would change no bit
+                // w0 has one nonzero term (lane 0's): its butterfly would change no bit.  The
+                // consts' second slot (c1, a sum of zeros) carries n_eff
                 c0 = xor_sum(c0, 64);
                 c5 = xor_sum(c5, 64);
+                ne = xor_max_i(ne, 64);
                 if (lane == 0) {
                     red[i][0] = c0;
-                    red[i][1] = c1;
+                    red[i][1] = (double)ne;
                     red[i][2] = c5;
                     red[i][3] = w0;
                 }
@@ -602,8 +628,9 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
 // option kernel helpers
 // ----------------------------------------------------------------------------------------------
 struct Consts {
-    double c0, c1, c5, w0, a, b, eb, ea;
+    double c0, ne, c5, w0, a, b, eb, ea;   // ne: the table's n_eff (tail_keep), as a double
 };
+
 
 // sum' of one option from the table constants and its angle sum (k = 0 term:
 // chi_0 = e^d - e^c, psi_0 = d - c, double_heston.py:142-143,154-155).
@@ -611,7 +638,7 @@ __device__ __forceinline__ double option_sum(const Consts& C, bool is_call, doub
                                              double xK, double exK, double sum) {
     const double v0 = is_call ? (S0 * (C.eb - exK) - K * (C.b - xK))
                               : (K * (xK - C.a) - S0 * (exK - C.ea));
-    const double cst = is_call ? (C.c0 - K * C.c1) : C.c5;
+    const double cst = is_call ? C.c0 : C.c5;      // (the call's - K c1 term: c1 == 0 exactly)
     return cst + C.w0 * v0 - exK * sum;
 }
 
@@ -889,7 +916,7 @@ __device__ __forceinline__ void tile_sums_r(const PriceArgs& A, int64_t p, const
                                             double S0, double disc, int nopt, int G, int tpt,
                                             int t, bool active, const TileLds& L, double* red,
                                             const double2* sct) {
-    const int N = A.N;
+    const int Ne = (int)C.ne;                     // the table's kept terms: k < n_eff
     const int R = min(RT, max(nopt, 1));
     const int ngroups = (nopt + R - 1) / R;
     const int groups_per_pass = max(1, tpt / G);
@@ -912,7 +939,7 @@ __device__ __forceinline__ void tile_sums_r(const PriceArgs& A, int64_t p, const
         }
         double sm[RT];
         if (pass == 0) DH_STAMP(A, 9);
-        angle_sums_r<RT>(1 + gl, G, N, dx, cs, ss, L.tu, L.t26, sct, sm);
+        angle_sums_r<RT>(1 + gl, G, Ne, dx, cs, ss, L.tu, L.t26, sct, sm);
         if (pass == 0) DH_STAMP(A, 10);
         if (lds_red) {
             if (gvalid) {
@@ -1041,7 +1068,8 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     if (active) {
         const double* tw = A.table + q * (int64_t)N;     // row-major (never tiled here)
         const double piba = dh::kPi / ba;
-        for (int k = t; k < N; k += TPT) {
+        const int ne = (int)C.ne;                        // terms past n_eff are never read
+        for (int k = t; k < ne; k += TPT) {
             const double w = tw[k];
             const double u = k * piba;
             const double T2 = k == 0 ? 0.0 : w * P.S0 * dh::drcp(1.0 + u * u);
@@ -1194,7 +1222,8 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A_, 
     // segments of kAnchor terms (the first starts exact at k = 1; later ones re-anchor on an
     // exact (k, k - 1) pair), two terms per iteration with x_k / x_{k-1} swapping registers
     const int N = A.N;
-    for (int k0 = 1; k0 < N; k0 += kAnchor) {
+    const int ne = (int)C.ne;                        // the table's kept terms: k < n_eff
+    for (int k0 = 1; k0 < ne; k0 += kAnchor) {
         if (k0 > 1) {
             const double uk = k0 * piba;
 #pragma unroll
@@ -1204,7 +1233,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A_, 
                 sp[j] = sn[j] * cs[j] - c[j] * ss[j];
             }
         }
-        const int kend = min(N, k0 + kAnchor);
+        const int kend = min(ne, k0 + kAnchor);
         int k = k0;
         double wa = active ? tw[k * kTabTile] : 0.0;
         for (; k + 1 < kend; k += 2) {
@@ -1307,6 +1336,7 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
     extern __shared__ __attribute__((aligned(16))) double2 gtab[];   // [TB][N] (T2, T6)
     __shared__ double shc[TB][kTabC];
     __shared__ double ks[TB][3];                     // c0, c5, w0
+    __shared__ int kne[TB];                          // n_eff (tail_keep)
     __shared__ double osse[TB][kSmallTile], obad[TB][kSmallTile];
     __shared__ double2 sct[dh::kMathTab];
     dh::load_math_tables(sct, 0);                    // synchronised by the first barrier
@@ -1316,7 +1346,6 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
     const int tpp = tabs_per_p(A);
     const int64_t n_q = A.np * tpp;
     const int S = TPT / OP;                          // k-blocks per option
-    const int Lk = (N - 1 + S - 1) / S;              // terms per k-block
     const int it = t / TPT, sub = t % TPT;           // CF phase: table slot, thread in table
     const int io = t / TPT, oo = (t % TPT) / S, jj = t % S;   // option phase: table, option, k-block
     for (int64_t b0 = (int64_t)blockIdx.x * TB; b0 < n_q; b0 += (int64_t)gridDim.x * TB) {
@@ -1334,7 +1363,9 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
                 for (int j = 0; j < 16; ++j) cc[j] = c[6 + j];
             }
             double2* tb = gtab + (size_t)it * N;
+            const double delta = tail_delta(S0, c[1] - a, N);
             double c0 = 0.0, c5 = 0.0, w0 = 0.0;
+            int ne = 0;
             table_entries<TPT>(CC, sub, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
                 if (k == 0) {
                     w0 = 0.5 * w;
@@ -1346,14 +1377,17 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
                 const double cb = (k & 1) ? -1.0 : 1.0;
                 c0 += T2 * eb * cb;
                 c5 += T2 * ea;
+                ne = max(ne, tail_keep(k, T2, delta));
             });
             c0 = xor_sum(c0, TPT);
             c5 = xor_sum(c5, TPT);
             w0 = xor_sum(w0, TPT);                   // one nonzero term (thread 0's)
+            ne = xor_max_i(ne, TPT);
             if (sub == 0) {
                 ks[it][0] = c0;
                 ks[it][1] = c5;
                 ks[it][2] = w0;
+                kne[it] = ne;
             }
         }
         __syncthreads();
@@ -1379,7 +1413,10 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
             dh::dsincos_t(th, sct, &st, &ct);
             const double c2 = 2.0 * ct;
             const double2* tb = gtab + (size_t)(tab_ok ? io : 0) * N;
-            const int k_lo = 1 + jj * Lk, k_hi = min(N, k_lo + Lk);
+            // the kept terms k < n_eff in S k-blocks of Lk
+            const int ne = tab_ok ? kne[io] : 0;
+            const int Lk = (max(ne, 1) - 1 + S - 1) / S;
+            const int k_lo = 1 + jj * Lk, k_hi = min(ne, k_lo + Lk);
             double sc = 0.0, ss = 0.0;
             for (int k0 = k_lo; k0 < k_hi; k0 += kAnchor) {
                 double cx, sx;                                     // cos / sin (k0 th)
@@ -1439,7 +1476,7 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
         sum = xor_sum(sum, S);
         const int64_t p = A.p0 + (tab_ok ? q / tpp : 0);
         if (use && jj == 0) {
-            const Consts C{ks[io][0], 0.0, ks[io][1], ks[io][2], a, b, c[2], c[3]};
+            const Consts C{ks[io][0], 0.0, ks[io][1], ks[io][2], a, b, c[2], c[3]};   // ne unused
             const double price = c[29] * option_sum(C, A.call[m] != 0, S0, K, xK, ratio, sum);
             if (A.out) A.out[p * A.out_stride + A.perm[m]] = price;
             if (A.part_sse) {
@@ -1687,20 +1724,28 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const int w5 = (WV <= DH_FUSED_WAVES && nthr >= 192) ? nthr / 64 - 1 : 0;
     if (wv == 0 || wv == w5) {
         const bool f0 = wv == 0, f5 = wv == w5;
+        const double delta = tail_delta(S0, b - a, N);
         double c0 = 0.0, c5 = 0.0;
+        int ne = 0;                                  // n_eff (tail_keep), on wave 0 with c0
         for (int k = lane; k < N; k += 64) {
             if (k == 0) continue;
             const double T2 = L.t26[k].x;
             const double cb = (k & 1) ? -1.0 : 1.0;
-            if (f0) c0 += T2 * eb * cb;
+            if (f0) {
+                c0 += T2 * eb * cb;
+                ne = max(ne, tail_keep(k, T2, delta));
+            }
             if (f5) c5 += T2 * ea;
         }
-        if (f0) c0 = xor_sum(c0, 64);
+        if (f0) {
+            c0 = xor_sum(c0, 64);
+            ne = xor_max_i(ne, 64);
+        }
         if (f5) c5 = xor_sum(c5, 64);
         if (lane == 0) {
             if (f0) {
                 red[0][0] = c0;
-                red[1][0] = 0.0;
+                red[1][0] = (double)ne;
                 red[3][0] = w0s;
             }
             if (f5) red[2][0] = c5;

@@ -1,61 +1,95 @@
-"""Per-basic-block instruction mix of one kernel in a hipcc --save-temps .s file.
+#!/usr/bin/env python3
+"""Per-basic-block instruction counts of one kernel in the gfx950 assembly (`make asm` writes
+/tmp/dhcos_asm/dh_kernels-hip-amdgcn-amd-amdhsa-gfx950.s), with loops marked from their back
+edges: the static half of a VALU budget (multiply each block by its trip count).
 
-Usage: python tools/isa_blocks.py <file.s> <kernel-name-substring> [--min 40]
-Prints each basic block with >= --min instructions: label, #instr, #VALU, #fp64 VALU, #SALU,
-#LDS, #VMEM, backward-branch target (loops)."""
+usage: python tools/isa_blocks.py KERNEL_SUBSTRING [--asm FILE] [--min 1]
+"""
+import argparse
 import re
-import sys
+
+ASM = "/tmp/dhcos_asm/dh_kernels-hip-amdgcn-amd-amdhsa-gfx950.s"
+
+
+def classify(op):
+    if op.startswith("v_mfma"):
+        return "mfma"
+    if op.startswith("v_"):
+        return "valu"
+    if op.startswith("ds_"):
+        return "lds"
+    if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
+        return "vmem"
+    if op.startswith("s_waitcnt"):
+        return "wait"
+    if op.startswith(("s_cbranch", "s_branch")):
+        return "br"
+    if op.startswith("s_"):
+        return "salu"
+    return None
 
 
 def main():
-    path, name = sys.argv[1], sys.argv[2]
-    mn = int(sys.argv[sys.argv.index("--min") + 1]) if "--min" in sys.argv else 40
-    lines = open(path).read().splitlines()
-    start = None
-    for i, ln in enumerate(lines):
-        if re.match(r"^_Z\S*:", ln) and name in ln:
-            start = i
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kernel")
+    ap.add_argument("--asm", default=ASM)
+    ap.add_argument("--min", type=int, default=1, help="hide blocks with fewer VALU")
+    a = ap.parse_args()
+    lines = open(a.asm).read().split("\n")
+    start = next(i for i, l in enumerate(lines)
+                 if l.endswith(":") is False and a.kernel in l and l.split(":")[0].startswith("_Z")
+                 and not l.startswith("\t"))
+    name = lines[start].split(":")[0]
+    blocks, cur = [], {"label": "entry", "line": start, "n": {}, "ops": [], "targets": [],
+                       "comment": ""}
+    for i in range(start + 1, len(lines)):
+        l = lines[i]
+        if l.startswith(".Lfunc_end"):
             break
-    if start is None:
-        sys.exit("kernel not found")
-    blocks, cur, label = [], [], lines[start].rstrip(":")
-    order = {}
-    for ln in lines[start + 1:]:
-        if ln.startswith(".Lfunc_end"):
-            break
-        m = re.match(r"^(\.LBB\S+):", ln)
+        m = re.match(r"^(\.LBB\d+_\d+):(.*)", l)
         if m:
-            blocks.append((label, cur))
-            label, cur = m.group(1), []
+            blocks.append(cur)
+            cur = {"label": m.group(1), "line": i, "n": {}, "ops": [], "targets": [],
+                   "comment": m.group(2).strip()}
             continue
-        s = ln.strip()
-        if not s or s.startswith((";", ".", "//")):
+        s = l.strip()
+        if not s or s.startswith((";", ".")):
+            if s.startswith("; %bb") or "Loop" in s:
+                cur["comment"] += " " + s
             continue
-        cur.append(s)
-    blocks.append((label, cur))
-    for idx, (lb, _) in enumerate(blocks):
-        order[lb] = idx
-    tot = dict(n=0, valu=0, f64=0)
-    for idx, (lb, ins) in enumerate(blocks):
-        ops = [i.split()[0] for i in ins]
-        valu = [o for o in ops if o.startswith("v_")]
-        f64 = [o for o in valu if "f64" in o]
-        salu = [o for o in ops if o.startswith("s_")]
-        lds = [o for o in ops if o.startswith("ds_")]
-        vmem = [o for o in ops if o.startswith(("global_", "buffer_", "flat_", "scratch_"))]
-        back = ""
-        for i in ins:
-            m = re.match(r"s_(cbranch_\w+|branch)\s+(\.LBB\S+)", i)
-            if m and order.get(m.group(2), 1 << 30) <= idx:
-                back = f"loop->{m.group(2)}"
-        tot["n"] += len(ops)
-        tot["valu"] += len(valu)
-        tot["f64"] += len(f64)
-        if len(ops) >= mn or back:
-            trans = [o for o in valu if o.startswith(("v_rcp", "v_rsq", "v_sqrt", "v_exp", "v_log", "v_sin", "v_cos", "v_frexp", "v_ldexp"))]
-            print(f"{lb:22s} n={len(ops):5d} valu={len(valu):5d} f64={len(f64):5d} "
-                  f"trans={len(trans):3d} salu={len(salu):4d} lds={len(lds):3d} vmem={len(vmem):3d} {back}")
+        op = s.split()[0]
+        c = classify(op)
+        if c:
+            cur["n"][c] = cur["n"].get(c, 0) + 1
+            cur["ops"].append(op)
+        if c == "br":
+            t = s.split()[-1]
+            if t.startswith(".LBB"):
+                cur["targets"].append(t)
+    blocks.append(cur)
+    idx = {b["label"]: k for k, b in enumerate(blocks)}
+    loops = []
+    for k, b in enumerate(blocks):
+        for t in b["targets"]:
+            if t in idx and idx[t] <= k:
+                loops.append((idx[t], k))
+    print(name)
+    tot = {}
+    for k, b in enumerate(blocks):
+        for c, v in b["n"].items():
+            tot[c] = tot.get(c, 0) + v
+        depth = sum(1 for s, e in loops if s <= k <= e)
+        if b["n"].get("valu", 0) < a.min and not any(s == k for s, e in loops):
+            continue
+        head = "".join(f" [loop {s}-{e}]" for s, e in loops if s == k)
+        print(f"{k:4d} {b['label']:>12} line {b['line']:6d} depth {depth} "
+              f"valu {b['n'].get('valu', 0):4d} salu {b['n'].get('salu', 0):3d} "
+              f"lds {b['n'].get('lds', 0):3d} vmem {b['n'].get('vmem', 0):3d}{head} "
+              f"{b['comment'][:60]}")
     print("total", tot)
+    for s, e in loops:
+        v = sum(blocks[k]["n"].get("valu", 0) for k in range(s, e + 1))
+        print(f"loop {s}-{e}: {v} VALU over its blocks")
 
 
 if __name__ == "__main__":
