@@ -388,7 +388,7 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                 "data": "synthetic",
                 "config": {"workload": cfg["workload"], "param_sets": P, "options": M,
-                           "cos_terms": N, "prices_per_step": P * M,
+                           "cos_terms": N, "prices_per_step": P * M, "tail_cut": args.tail_cut,
                            "parallelism": f"independent batches per rank x{world}"},
                 "roofline": roofline}
         if cpu:
@@ -445,6 +445,9 @@ def main():
     ap.add_argument("--path", default="auto", choices=["auto", "split", "fused"],
                     help="request kernels (libdhcos dh_ctx_set_path): auto, table+option "
                          "launches, or one fused launch")
+    ap.add_argument("--tail-cut", default="on", choices=["on", "off"],
+                    help="adaptive tail of the angle sums (dh_ctx_set_tail_cut; off: every COS "
+                         "term summed, for A/B)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N > 1 "
                          "with several ranks on one GPU)")
@@ -474,6 +477,7 @@ def main():
     os.environ["DHCOS_DEVICE"] = str(local)
     _native.default_context().set_path({"auto": _native.PATH_AUTO, "split": _native.PATH_SPLIT,
                                         "fused": _native.PATH_FUSED}[args.path])
+    _native.default_context().set_tail_cut(args.tail_cut == "on")
     # a dedicated (non-null) stream: libdhcos launches on it and the HIP events time it
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
@@ -578,7 +582,7 @@ def main():
             "warmup": W_, "ms_per_step": dt / K_ * 1e3, "higher_is_better": True,
             "scaling": "strong" if cfg.get("strong") else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": cfg["workload"], "options": M, "cos_terms": N,
-                       "param_sets_per_step": S, "prices_per_step": prices_per_step,
+                       "tail_cut": args.tail_cut, "param_sets_per_step": S, "prices_per_step": prices_per_step,
                        "parallelism": f"independent requests per rank x{world}"},
             "roofline": roofline,
             "host_api_prices_per_sec": host_rate,

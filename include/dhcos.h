@@ -69,6 +69,10 @@ void* dh_ctx_stream(dh_ctx* ctx);
 /* Validation mode: when on, every option is priced by the per-term path in the reference's
  * operation order (own CF and sincos per COS term) instead of the shared-table fast path.   */
 int dh_ctx_set_exact(dh_ctx* ctx, int on);
+/* Adaptive tail of the fast path's angle sums (on by default): a table's COS terms past the last
+ * one with |T2_k| > 2^-72 S0 / ((b - a)(1 + (b - a)/pi) N) are not summed, which moves no price by
+ * more than 2^-64 of its k = 0 term.  Off: every term k < N is summed (A/B, tests). */
+int dh_ctx_set_tail_cut(dh_ctx* ctx, int on);
 /* Request kernels of the fast path.  AUTO (default): one fused launch per request when every
  * maturity group fits one tile (<= 256 options), except small tiles in large calls (generator
  * grids: a COS-table launch then the lane-per-option-group kernel); otherwise the table launch
@@ -225,6 +229,13 @@ int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* c
                 int64_t n_samples, const double* lo, const double* hi, int n_opt, double alpha,
                 double spot0, double ret_mu, double ret_sigma, double noise_sigma, double* params,
                 double* spots, double* noise);
+/* The generator's host arithmetic after pricing (synthetic_generator.py:141-157), per sample i
+ * and option j of [n_samples][n_opt] row-major arrays: market = model + noise * model, loss[i] =
+ * mean_j ((model - market) / market)^2 formed as np.mean forms it (bit for bit), strikes =
+ * (k_rel[j] * spots[i]) / 100.  Host code (threads), no device work.                      */
+int dh_gen_assemble(const double* model, const double* noise, const double* spots,
+                    const double* k_rel, int64_t n_samples, int n_opt, double* market,
+                    double* loss, double* strikes);
 
 /* ---- paired pricing: option i under param set i ------------------------------------------- */
 /* out[i] = price of (K[i], T[i], is_call[i]) under params[i]; replaces a loop of single

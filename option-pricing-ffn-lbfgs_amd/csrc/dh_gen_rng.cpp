@@ -367,3 +367,76 @@ extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss
     *cached_gauss = g.gauss;
     return DH_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// dh_gen_assemble: the generator's per-sample host arithmetic after pricing
+// (synthetic_generator.py:141-157), one pass over the batch on a worker team:
+//   market = model + noise * model            (:141-142, NumPy's two roundings, no contraction)
+//   rel    = (model - market) / market;  loss = mean(rel ** 2)          (:154-157)
+//   strike = (K_rel * spot) / 100             (the columnar output's absolute strikes)
+// loss is np.mean over a sample's options exactly as NumPy (2.x) forms it: add.reduce's pairwise
+// sum of the row (plain below 8 terms, eight accumulators up to 128, halving above), then one
+// division by the count (tests/test_generator_rng.py holds it to np.mean bit for bit).
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+double np_pairwise_sum(const double* a, int64_t n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int64_t i = 0; i < n; ++i) res += a[i];
+        return res;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int64_t i = 8;
+        for (; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_pairwise_sum(a, n2) + np_pairwise_sum(a + n2, n - n2);
+}
+
+}  // namespace
+
+extern "C" int dh_gen_assemble(const double* model, const double* noise, const double* spots,
+                               const double* k_rel, int64_t n_samples, int n_opt, double* market,
+                               double* loss, double* strikes) {
+    if (n_samples < 0 || n_opt < 0) return DH_E_ARG;
+    if (n_samples == 0) return DH_OK;
+    if (!loss) return DH_E_ARG;
+    if (n_opt == 0) {
+        for (int64_t i = 0; i < n_samples; ++i) loss[i] = NAN;   // mean of nothing (NumPy: nan)
+        return DH_OK;
+    }
+    if (!model || !noise || !spots || !k_rel || !market || !loss || !strikes) return DH_E_ARG;
+    auto sweep = [&](int64_t i0, int64_t i1) {
+        std::vector<double> sq(n_opt);
+        for (int64_t i = i0; i < i1; ++i) {
+            const double* md = model + i * n_opt;
+            const double* nz = noise + i * n_opt;
+            double* mk = market + i * n_opt;
+            double* st = strikes + i * n_opt;
+            for (int j = 0; j < n_opt; ++j) {
+                const double m = md[j] + nz[j] * md[j];
+                const double r = (md[j] - m) / m;
+                mk[j] = m;
+                sq[j] = r * r;
+                st[j] = (k_rel[j] * spots[i]) / 100.0;
+            }
+            loss[i] = np_pairwise_sum(sq.data(), n_opt) / (double)n_opt;
+        }
+    };
+    if (n_samples < kSplitMin) {
+        sweep(0, n_samples);
+        return DH_OK;
+    }
+    Team team((int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    const int nt = team.size();
+    team.run([&](int w) { sweep(n_samples * w / nt, n_samples * (w + 1) / nt); });
+    return DH_OK;
+}

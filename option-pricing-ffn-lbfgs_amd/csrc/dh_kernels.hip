@@ -111,6 +111,8 @@ struct PriceArgs {
                             // has finished (*live_count == 0), else null
     const double* pre;      // fused kernel on large grids: [tables][kTabC] prologue constants
                             // formed by table_prologue_kernel ahead of it, else null
+    double tail;            // tail_delta's scale: kTailScale, or -1 (dh_ctx_set_tail_cut(0): every
+                            // term summed); set by launch_price
 };
 
 // w_k of table q sits at table_w(A, q)[k * table_step(A)].  The small-tile option kernel has one
@@ -428,8 +430,9 @@ __global__ __launch_bounds__(kBlock) void table_prologue_kernel(PriceArgs A, int
 // keeps ~26% of its terms, at N = 256 ~46%, at N = 128 ~97%.  Every path forms n_eff from the
 // same T2_k values with the same expressions, so fused and split keep their identical bits.
 // NaN / inf entries (and a NaN delta) always count as kept: a NaN still reaches the price.
-__device__ __forceinline__ double tail_delta(double S0, double ba, int N) {
-    return 0x1.0p-72 * S0 / (ba * (1.0 + ba * (1.0 / dh::kPi)) * (double)N);
+constexpr double kTailScale = 0x1.0p-72;
+__device__ __forceinline__ double tail_delta(double scale, double S0, double ba, int N) {
+    return scale * S0 / (ba * (1.0 + ba * (1.0 / dh::kPi)) * (double)N);
 }
 __device__ __forceinline__ int tail_keep(int k, double T2, double delta) {
     return fabs(T2) <= delta ? 0 : k + 1;
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             const int g0 = (int)c[27], gn = has ? (int)c[28] : 0;
             double* t2 = t2s + (TPT > 64 ? slot * N : 0);
             double c0 = 0.0, c5 = 0.0, w0 = 0.0;
-            const double delta = tail_delta(S0, b - a, N);
+            const double delta = tail_delta(A.tail, S0, b - a, N);
             int ne = 0;
             if (has) {
                 dh::CfConsts CC;
@@ -1363,7 +1366,7 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
                 for (int j = 0; j < 16; ++j) cc[j] = c[6 + j];
             }
             double2* tb = gtab + (size_t)it * N;
-            const double delta = tail_delta(S0, c[1] - a, N);
+            const double delta = tail_delta(A.tail, S0, c[1] - a, N);
             double c0 = 0.0, c5 = 0.0, w0 = 0.0;
             int ne = 0;
             table_entries<TPT>(CC, sub, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
@@ -1724,7 +1727,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const int w5 = (WV <= DH_FUSED_WAVES && nthr >= 192) ? nthr / 64 - 1 : 0;
     if (wv == 0 || wv == w5) {
         const bool f0 = wv == 0, f5 = wv == w5;
-        const double delta = tail_delta(S0, b - a, N);
+        const double delta = tail_delta(A.tail, S0, b - a, N);
         double c0 = 0.0, c5 = 0.0;
         int ne = 0;                                  // n_eff (tail_keep), on wave 0 with c0
         for (int k = lane; k < N; k += 64) {
@@ -2043,6 +2046,7 @@ struct dh_ctx {
     bool attr_set = false;
     dh_ctx_view view;          // resident cos_table_kernel<64/128/256> blocks, whole chip
     int exact = 0;          // validation mode: every option through the per-term exact path
+    int tail_cut = 1;       // adaptive tail of the angle sums (tail_delta; dh_ctx_set_tail_cut)
     int path = DH_PATH_AUTO;   // fused / split request kernels (dh_ctx_set_path)
     int last_path = 0;         // kernels of the last fast-path request (dh_ctx_last_path)
     int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
@@ -2279,7 +2283,9 @@ int launch_gen(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st, int TB) {
 // Table kernel then option kernel per chunk of param sets; the chunk keeps the table workspace
 // within kTableBudget (L2/MALL-resident between the two launches).  Requests whose maturity
 // groups are single tiles may instead run as one fused launch (ctx->path).
-int launch_price(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
+int launch_price(dh_ctx* ctx, const PriceArgs& A_in, hipStream_t st) {
+    PriceArgs A0 = A_in;
+    A0.tail = ctx->tail_cut ? kTailScale : -1.0;
     const int64_t tasks_per_p = A0.paired ? 1 : A0.n_tiles;
     if (A0.P * tasks_per_p == 0) return DH_OK;
     if (A0.exact) return launch_exact(ctx, A0, st);
@@ -2516,6 +2522,12 @@ int dh_ctx_last_path(dh_ctx* ctx) { return ctx ? ctx->last_path : DH_E_ARG; }
 int dh_ctx_set_exact(dh_ctx* ctx, int on) {
     if (!ctx) return fail(DH_E_ARG, "ctx is null");
     ctx->exact = on ? 1 : 0;
+    return DH_OK;
+}
+
+int dh_ctx_set_tail_cut(dh_ctx* ctx, int on) {
+    if (!ctx) return fail(DH_E_ARG, "ctx is null");
+    ctx->tail_cut = on ? 1 : 0;
     return DH_OK;
 }
 

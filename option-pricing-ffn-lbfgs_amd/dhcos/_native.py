@@ -58,6 +58,7 @@ SIGNATURES = {
     "dh_ctx_synchronize": (C.c_int, [_vp]),
     "dh_ctx_stream": (_vp, [_vp]),
     "dh_ctx_set_exact": (C.c_int, [_vp, C.c_int]),
+    "dh_ctx_set_tail_cut": (C.c_int, [_vp, C.c_int]),
     "dh_ctx_set_path": (C.c_int, [_vp, C.c_int]),
     "dh_ctx_last_path": (C.c_int, [_vp]),
     "dh_ctx_debug_stamps": (C.c_int, [_vp, C.c_int]),
@@ -81,6 +82,7 @@ SIGNATURES = {
     "dh_gen_draw": (C.c_int, [C.POINTER(C.c_uint32), _i32p, _i32p, _dp, C.c_int64, _dp, _dp,
                               C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                               _dp, _dp, _dp]),
+    "dh_gen_assemble": (C.c_int, [_dp, _dp, _dp, _dp, C.c_int64, C.c_int, _dp, _dp, _dp]),
     "dh_price_batch": (C.c_int, [_vp, _dp, C.c_int64, _dp, _dp, _i8p, C.c_int, C.c_int,
                                  C.c_double, _dp]),
     "dh_loss_batch": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp, _i8p, _dp, C.c_int, C.c_double,
@@ -190,6 +192,10 @@ class Context:
     def set_exact(self, on: bool):
         """Validation mode: price every option by the per-term reference-order path."""
         _check(load().dh_ctx_set_exact(self._h, 1 if on else 0))
+
+    def set_tail_cut(self, on: bool):
+        """Adaptive tail of the angle sums (default on); off sums every term k < N."""
+        _check(load().dh_ctx_set_tail_cut(self._h, 1 if on else 0))
 
     def set_path(self, path: int):
         """Request kernels: PATH_AUTO (default), PATH_SPLIT (table + option launches) or
@@ -572,6 +578,20 @@ def gen_draw(n_samples, lo, hi, n_opt, alpha, spot0, ret_mu, ret_sigma, noise_si
     return params, spots, noise
 
 
+def gen_assemble(model, noise, spots, k_rel):
+    """dh_gen_assemble: the generator's market prices, per-sample losses (np.mean's bits) and
+    absolute strikes from [n, m] model prices and noise.  -> (market, loss, strikes)."""
+    model, noise = _f64(model), _f64(noise)
+    spots, k_rel = _f64(spots), _f64(k_rel)
+    n, m = model.shape
+    if noise.shape != (n, m) or spots.shape != (n,) or k_rel.shape != (m,):
+        raise NativeError("gen_assemble: shape mismatch")
+    market, loss, strikes = np.empty((n, m)), np.empty(n), np.empty((n, m))
+    _check(load().dh_gen_assemble(_ptr(model), _ptr(noise), _ptr(spots), _ptr(k_rel), n, m,
+                                  _ptr(market), _ptr(loss), _ptr(strikes)))
+    return market, loss, strikes
+
+
 _tls = threading.local()
 
 
@@ -611,7 +631,7 @@ def default_context(device: int | None = None) -> Context:
     return ctx
 
 
-__all__ = ["gen_draw", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
+__all__ = ["gen_draw", "gen_assemble", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "MAX_N_PER_TERM",
            "STRIKE_ABSOLUTE",
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN", "LIB_PATH",

@@ -158,17 +158,17 @@ def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose
     # the columnar output keeps the dates as one '<U10' array: 10^6 Python strings were most of
     # the host time of a 1M-sample run (profiles/r03_generator_e2e.json)
     dates = trading_dates_array(n_samples) if as_arrays else trading_dates(n_samples)
-    market = model + noise * model                                   # (:141-142)
-    rel = (model - market) / market
-    losses = np.mean(rel ** 2, axis=1)                               # (:154-157)
     names = list(PARAM_RANGES.keys())
     Krel = np.tile(STRIKES_PCT, len(MATURITIES))
     Tg = np.repeat(MATURITIES, len(STRIKES_PCT))
+    # market = model + noise * model (:141-142), loss = mean(((model - market)/market)^2)
+    # (:154-157) and the absolute strikes in one native pass, NumPy's bits
+    # (_native.gen_assemble: dh_gen_assemble)
+    market, losses, strikes = _native.gen_assemble(model, noise, spots, Krel)
     if as_arrays:
         result = dict(dates=dates, spot=spots, risk_free=RISK_FREE, params=params,
                       param_names=names, market_prices=market, model_prices=model,
-                      strikes=(Krel[None, :] * spots[:, None]) / 100.0,
-                      maturities=Tg, final_loss=losses)
+                      strikes=strikes, maturities=Tg, final_loss=losses)
         if save_path:
             np.savez(save_path if save_path.endswith(".npz") else save_path + ".npz",
                      **{k: v for k, v in result.items() if k != "param_names"},

@@ -103,3 +103,23 @@ def test_native_draw_any_stream_position(pos):
     for a, b in zip(got, want):
         assert np.array_equal(a, b)
     assert np.array_equal(after_got[1], after_want[1]) and after_got[2:] == after_want[2:]
+
+
+@pytest.mark.parametrize("n,m", [(5, 15), (5000, 15), (300, 1), (300, 7), (300, 8), (300, 9),
+                                 (200, 32), (100, 129), (50, 300)])
+def test_native_assemble_equals_numpy(n, m):
+    """dh_gen_assemble (market = model + noise model, loss = np.mean of rel^2, absolute strikes)
+    against the NumPy expressions of the reference (synthetic_generator.py:141-157), bit for bit,
+    below and above the worker-team threshold and across np.mean's pairwise-sum block sizes."""
+    from dhcos import _native
+    rs = np.random.RandomState(n + m)
+    model = np.abs(rs.standard_normal((n, m))) * 10 + 1e-3
+    noise = rs.normal(0, 0.02, (n, m))
+    spots = 100 * np.exp(rs.normal(0, 0.1, n))
+    k_rel = rs.uniform(80, 120, m)
+    market, loss, strikes = _native.gen_assemble(model, noise, spots, k_rel)
+    want_mkt = model + noise * model
+    assert np.array_equal(market, want_mkt)
+    assert np.array_equal(loss, np.array([np.mean(((model[i] - want_mkt[i]) / want_mkt[i]) ** 2)
+                                          for i in range(n)]))
+    assert np.array_equal(strikes, (k_rel[None, :] * spots[:, None]) / 100.0)

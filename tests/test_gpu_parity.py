@@ -552,6 +552,33 @@ def test_fast_path_matches_exact_mode_full_size(dh):
     assert rel_close(fast, exact, 1e-11, 1e-11).all(), np.max(np.abs(fast - exact))
 
 
+@pytest.mark.parametrize("N", [128, 512, 2048])
+def test_tail_cut_moves_prices_below_rounding(dh, N):
+    """The adaptive tail of the angle sums (dh_ctx_set_tail_cut): a table's terms
+    past its last |T2_k| > 2^-72 S0/((b-a)(1+(b-a)/pi)N) are dropped, provably < 2^-64 of each
+    price's k = 0 term.  Against the same kernels summing every term, the prices move by no more
+    than the shorter sums' own rounding (bound: 1e-13 K), and they still match the oracle.  (The
+    dropped terms sit below half an ulp of the running sums, so on these surfaces the two agree
+    bit for bit even though most terms are dropped at N = 512 / 2048: bench.py --tail-cut off
+    shows the time they take.)"""
+    from dhcos import _native
+    params, rec, K, T, call = _surface_case(17, P=4, M=2000, n_T=20, N=N)
+    ctx = _native.default_context()
+    surf = _native.Surface(ctx, K, T, call)
+    cut = surf.price(rec, N)
+    ctx.set_tail_cut(False)
+    try:
+        full = surf.price(rec, N)
+    finally:
+        ctx.set_tail_cut(True)
+    d = np.abs(cut - full)
+    print(f"N={N}: max |cut - full| {d.max():.3e}, changed {np.mean(d > 0):.3f} of prices")
+    assert np.all(d <= 1e-13 * K[None, :]), d.max()
+    for p in range(params.shape[0]):
+        want = O.price_many(params[p], 100.0, K, T, 0.03, call, N)
+        assert rel_close(cut[p], want, FID_RTOL, BAR_ATOL).all(), np.max(np.abs(cut[p] - want))
+
+
 def test_clamped_options_across_mask_words_and_tiles(dh):
     """The table kernel decides and prices clamp-widened options (double_heston.py:135-137) and
     the option kernel looks them up by a per-(p, group) bit mask.  One maturity group of 300
