@@ -18,7 +18,10 @@
 // so the global stream continues exactly where the reference's loop would leave it.  No FMA
 // contraction (the Makefile builds this file with -ffp-contract=off), libm log / sqrt as NumPy.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -249,6 +252,21 @@ class Team {
     bool stop_ = false;
 };
 
+// Worker threads of a draw / assembly call: $DHCOS_GEN_THREADS, else min(16, hardware threads)
+// (16: the GPU box's CPU share per GPU)
+int team_size() {
+    if (const char* e = std::getenv("DHCOS_GEN_THREADS")) {
+        const int v = std::atoi(e);
+        if (v > 0) return std::min(v, 256);
+    }
+    return (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 // Samples per chunk of the split draw (bounds its buffers), and below this many samples the
 // plain sequential loop
 constexpr int64_t kChunk = 1 << 16;
@@ -290,26 +308,94 @@ extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss
     } else {
         // Large draws in three passes per chunk of samples, the same operations on the same
         // values in the same order per value (so the same bits):
-        //   A (sequential): the MT19937 doubles (DoubleStream), the parameters and their AR(1)
+        //   A (this thread): the MT19937 doubles (DoubleStream), the parameters and their AR(1)
         //     blend, and for every gauss call either the accepted polar pair (x1, x2, r2) or a
         //     reference to the pair whose cached half it returns, exactly as has_gauss toggles;
-        //   B (parallel over pairs): next_gauss's log / sqrt / products;
-        //   C (parallel over samples): the noise; then the spot walk (sequential).
+        //   B (a helper thread): next_gauss's log / sqrt / products per pair;
+        //   C (the helper): the noise and the spot walk from the gauss values.
+        // A of chunk c + 1 runs while the helper does B and C of chunk c (two chunk slots), so a
+        // draw costs about pass A alone.  (A team of 4-16 workers for B / C was measured on the
+        // GPU box's EPYC host: B + C 0.05 -> 0.01 s per 1M samples, but pass A of the main
+        // thread 0.067 -> 0.12-0.16 s; one overlapped helper keeps A at its single-thread speed.)
+        struct Slot {
+            std::vector<double> px1, px2, pr2, gn, gc;      // per pair: inputs, f x2, f x1
+            // per sample: its first new pair in the chunk, and whether its first gauss call
+            // returns the value cached before it (the previous pair's f x1, or `pending`)
+            std::vector<int32_t> first;
+            std::vector<uint8_t> cached;
+            int64_t c0 = 0, c1 = 0;
+            int32_t np = 0;
+            bool full = false;                              // A done, B + C pending
+        };
         const int64_t per = (int64_t)n_opt + 1;             // gauss calls per sample, at most
-        const int64_t cap = std::min(n_samples, kChunk) * per;
-        std::vector<double> px1(cap), px2(cap), pr2(cap), gn(cap), gc(cap);
-        // per sample: its first new pair in the chunk, and whether its first gauss call returns
-        // the value cached before it (the previous pair's f x1, or `pending` at pair -1)
-        std::vector<int32_t> first(kChunk);
-        std::vector<uint8_t> cached(kChunk);
+        const int64_t cs = std::min(n_samples, kChunk);
+        Slot slots[2];
+        for (Slot& sl : slots) {
+            sl.px1.resize(cs * per);
+            sl.px2.resize(cs * per);
+            sl.pr2.resize(cs * per);
+            sl.gn.resize(cs * per);
+            sl.gc.resize(cs * per);
+            sl.first.resize(cs);
+            sl.cached.resize(cs);
+        }
+        std::mutex mu;
+        std::condition_variable cv;
+        bool produced = false;
         double pending = g.gauss;                           // the value cached at entry
-        Team team((int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+        double t_a = 0.0;                                   // $DHCOS_GEN_TIMING
+        const double t_start = now_s();
+        auto consume = [&](Slot& sl) {                      // B and C of one chunk
+            for (int32_t k = 0; k < sl.np; ++k)
+                pair_values(sl.px1[k], sl.px2[k], sl.pr2[k], sl.gn[k], sl.gc[k]);
+            auto value = [&](int64_t r, int c) {            // gauss call c of chunk sample r
+                const int32_t f = sl.first[r];
+                if (sl.cached[r]) {
+                    if (c == 0) return f == 0 ? pending : sl.gc[f - 1];
+                    --c;
+                }
+                return (c & 1) ? sl.gc[f + c / 2] : sl.gn[f + c / 2];
+            };
+            for (int64_t i = sl.c0; i < sl.c1; ++i) {
+                const int64_t r = i - sl.c0;
+                if (i > 0) spot = spot * (1.0 + (ret_mu + ret_sigma * value(r, 0)));
+                spots[i] = spot;
+                const int c00 = i > 0 ? 1 : 0;
+                double* z = noise + i * n_opt;
+                for (int j = 0; j < n_opt; ++j) z[j] = 0.0 + noise_sigma * value(r, c00 + j);
+            }
+            if (sl.np > 0) pending = sl.gc[sl.np - 1];      // cached into the next chunk if
+        };                                                  // has_gauss is set
+        std::thread helper([&] {
+            for (int64_t c = 0;; ++c) {
+                Slot& sl = slots[c & 1];
+                {
+                    std::unique_lock<std::mutex> l(mu);
+                    cv.wait(l, [&] { return sl.full || produced; });
+                    if (!sl.full) return;
+                }
+                consume(sl);
+                {
+                    std::lock_guard<std::mutex> l(mu);
+                    sl.full = false;
+                }
+                cv.notify_all();
+            }
+        });
         DoubleStream ds(g);
-        for (int64_t c0 = 0; c0 < n_samples; c0 += kChunk) {
-            const int64_t c1 = std::min(n_samples, c0 + kChunk);
+        int64_t c = 0;
+        for (int64_t c0 = 0; c0 < n_samples; c0 += kChunk, ++c) {
+            Slot& sl = slots[c & 1];
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [&] { return !sl.full; });
+            }
+            const double t0 = now_s();
+            sl.c0 = c0;
+            sl.c1 = std::min(n_samples, c0 + kChunk);
             int32_t np = 0;
             int hg = g.has_gauss;
-            for (int64_t i = c0; i < c1; ++i) {             // A
+            for (int64_t i = sl.c0; i < sl.c1; ++i) {       // A
                 double* p = params + i * 13;
                 for (int j = 0; j < 13; ++j) p[j] = lo[j] + range[j] * ds.next();   // :100-102
                 if (i > 0) {
@@ -321,44 +407,32 @@ extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss
                 // each serving two calls (f x2 now, f x1 cached for the next)
                 const int calls = n_opt + (i > 0 ? 1 : 0);
                 const int fresh = calls - hg;
-                first[i - c0] = np;
-                cached[i - c0] = (uint8_t)hg;
+                sl.first[i - sl.c0] = np;
+                sl.cached[i - sl.c0] = (uint8_t)hg;
                 const int k = (fresh + 1) / 2;
-                ds.pairs(k, px1.data() + np, px2.data() + np, pr2.data() + np);
+                ds.pairs(k, sl.px1.data() + np, sl.px2.data() + np, sl.pr2.data() + np);
                 np += k;
                 hg = fresh > 0 ? (fresh & 1) : hg - calls;
             }
             g.has_gauss = hg;
-            const int nt = team.size();
-            team.run([&](int w) {                           // B
-                for (int64_t k = (int64_t)np * w / nt; k < (int64_t)np * (w + 1) / nt; ++k)
-                    pair_values(px1[k], px2[k], pr2[k], gn[k], gc[k]);
-            });
-            // gauss call c of sample i (chunk-relative r)
-            auto value = [&](int64_t r, int c) {
-                const int32_t f = first[r];
-                if (cached[r]) {
-                    if (c == 0) return f == 0 ? pending : gc[f - 1];
-                    --c;
-                }
-                return (c & 1) ? gc[f + c / 2] : gn[f + c / 2];
-            };
-            const int64_t ns = c1 - c0;
-            team.run([&](int w) {                           // C: noise
-                for (int64_t r = ns * w / nt; r < ns * (w + 1) / nt; ++r) {
-                    const int64_t i = c0 + r;
-                    const int c00 = i > 0 ? 1 : 0;
-                    double* z = noise + i * n_opt;
-                    for (int j = 0; j < n_opt; ++j) z[j] = 0.0 + noise_sigma * value(r, c00 + j);
-                }
-            });
-            for (int64_t i = c0; i < c1; ++i) {             // C: spots
-                if (i > 0) spot = spot * (1.0 + (ret_mu + ret_sigma * value(i - c0, 0)));
-                spots[i] = spot;
+            sl.np = np;
+            t_a += now_s() - t0;
+            {
+                std::lock_guard<std::mutex> l(mu);
+                sl.full = true;
             }
-            if (np > 0) pending = gc[np - 1];               // cached into the next chunk if
-        }                                                   // has_gauss is set
+            cv.notify_all();
+        }
+        {
+            std::lock_guard<std::mutex> l(mu);
+            produced = true;
+        }
+        cv.notify_all();
+        helper.join();
         ds.sync();
+        if (std::getenv("DHCOS_GEN_TIMING"))
+            std::fprintf(stderr, "dh_gen_draw: %lld samples: pass A %.4f s, total %.4f s\n",
+                         (long long)n_samples, t_a, now_s() - t_start);
         g.gauss = g.has_gauss ? pending : 0.0;
     }
     std::memcpy(mt_key, g.key, sizeof(g.key));
@@ -435,7 +509,7 @@ extern "C" int dh_gen_assemble(const double* model, const double* noise, const d
         sweep(0, n_samples);
         return DH_OK;
     }
-    Team team((int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    Team team(team_size());
     const int nt = team.size();
     team.run([&](int w) { sweep(n_samples * w / nt, n_samples * (w + 1) / nt); });
     return DH_OK;
