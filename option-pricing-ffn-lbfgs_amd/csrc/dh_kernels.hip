@@ -239,11 +239,118 @@ __device__ __forceinline__ double xor_sum(double s, int width) {
     return s;
 }
 
+// Adaptive tail of the angle sums.  A table's terms k >= n_eff are not summed, n_eff - 1 being
+// the last k >= 1 with |T2_k| > tail_delta.  Past it |T6_k| = |T2_k| / u_k <= |T2_k| (b - a)/pi,
+// so the dropped part of S is at most (1 + (b - a)/pi) N delta = 2^-72 S0/(b - a), and a price
+// moves by at most e^{-rT} e^{xK} 2^-72 S0/(b - a) = e^{-rT} 2^-72 K/(b - a): below 2^-64 of its
+// own k = 0 term e^{-rT} w0 V0 (w0 = 1/(b - a); V0 >= 0.0048 K because the log-strike lies at
+// least 0.1 inside [a, b] -- clamp-widened options take the per-term path), i.e. far inside the
+// price's rounding.  The characteristic function decays like exp(-c u): at N = 512 (C3) a table
+// keeps ~26% of its terms, at N = 256 ~46%, at N = 128 ~97%.  Every path forms n_eff from the
+// same T2_k values with the same expressions, so fused and split keep their identical bits.
+// NaN / inf entries (and a NaN delta) always count as kept: a NaN still reaches the price.
+constexpr double kTailScale = 0x1.0p-72;
+__device__ __forceinline__ double tail_delta(double scale, double S0, double ba, int N) {
+    return scale * S0 / (ba * (1.0 + ba * (1.0 / dh::kPi)) * (double)N);
+}
+__device__ __forceinline__ int tail_keep(int k, double T2, double delta) {
+    return fabs(T2) <= delta ? 0 : k + 1;
+}
+__device__ __forceinline__ int xor_max_i(int v, int width) {
+    for (int off = 1; off < width; off <<= 1) v = max(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// Certified end of a table's CF entries.  For one Heston factor, conditioning on its variance
+// path leaves a Gaussian part with variance (1 - rho^2) I (I = the integrated variance), so
+// |phi_factor(u)| <= E[exp(-s I)] with s = u^2 (1 - rho^2) / 2: the CIR Laplace transform
+// exp(A(s) - B(s) v0), which decreases in u; the jump factor's modulus is <= 1 (lambda >= 0) and
+// the drift's is 1.  So |T2_k| <= 2 S0 M(u_k) / ((b - a)(1 + u_k^2)) =: bound(k), decreasing in
+// k, and from the first k with bound(k) <= delta / 2 (tail_delta) on every entry would be dropped
+// by the tail cut anyway: the CF is not evaluated there (K_cf, prologue slot 30).  The bound
+// follows |phi| closely: at N = 512 (C3) K_cf is ~7 terms past n_eff, ~28% of N
+// (tests/test_cf_cut_bound.py checks the bound against the oracle's CF).
+// The test runs in fp32 (native-rate transcendentals; its errors, ~1e-6 relative on log values
+// of magnitude < 1e3 near the threshold, sit far inside the 0.01 log-margin it keeps) on the
+// candidates k_j = (j + 1) ceil(N / 64), j < 64: K_cf is the first that passes (else N).  The
+// one-lane scan (table_prologue) and the wave's ballot (table_prologue_wave) test the same
+// candidates with the same bits, so they pick the same one.  Series of N < 512 terms are not
+// cut: at N = 128 (C1, C5) almost every term lies inside the bound, and at N = 256 the CF entries
+// are one per thread, so the halved CF work bought nothing while the test lengthened C2's
+// latency-bound prologue (12.1 -> 12.9 us; C4 unchanged).  Parameters outside the model's domain
+// (kappa, sigma, T <= 0, theta, v0, lambda < 0, |rho| > 1, NaN) and a disabled tail cut
+// (delta < 0) are not cut either.
+constexpr int kCfCutMinN = 512;
+
+__device__ __forceinline__ float cir_log_laplace(float s, float tau, float v0, float kap,
+                                                 float th, float sig) {
+#pragma clang fp contract(off)
+    const float s2 = sig * sig;
+    const float g = sqrtf(kap * kap + 2.0f * s2 * s);
+    const float e = expf(-(g * tau));
+    const float den = (g + kap) * (1.0f - e) + 2.0f * g * e;
+    const float B = 2.0f * s * (1.0f - e) / den;
+    const float A = (2.0f * kap * th / s2) * (logf(2.0f * g) + 0.5f * (kap - g) * tau - logf(den));
+    return A - B * v0;
+}
+
+__device__ __forceinline__ bool cf_cut_domain(const dh::Params& P, double T, double delta, int N) {
+    return N >= kCfCutMinN && delta > 0.0 &&
+           P.k1 > 0.0 && P.t1 >= 0.0 && P.s1 > 0.0 && P.v01 >= 0.0 && fabs(P.r1) <= 1.0 &&
+           P.k2 > 0.0 && P.t2 >= 0.0 && P.s2 > 0.0 && P.v02 >= 0.0 && fabs(P.r2) <= 1.0 &&
+           P.lam >= 0.0 && T > 0.0 && P.S0 > 0.0;
+}
+
+// log(delta / 2) less the margin: the candidates' threshold (one double log per table)
+__device__ __forceinline__ float cf_cut_threshold(double delta) {
+    return (float)log(0.5 * delta) - 0.01f;
+}
+
+// bound(k) <= delta / 2 with the margin, in logs, fp32
+__device__ __forceinline__ bool cf_cut_passes(const dh::Params& P, float T, float ba, float thr,
+                                              int k) {
+#pragma clang fp contract(off)
+    const float u = (float)k * (3.14159265f / ba);
+    const float u2 = u * u;
+    const float lm =
+        cir_log_laplace(0.5f * u2 * (1.0f - (float)P.r1 * (float)P.r1), T, (float)P.v01,
+                        (float)P.k1, (float)P.t1, (float)P.s1) +
+        cir_log_laplace(0.5f * u2 * (1.0f - (float)P.r2 * (float)P.r2), T, (float)P.v02,
+                        (float)P.k2, (float)P.t2, (float)P.s2);
+    return logf(2.0f * (float)P.S0 / (ba * (1.0f + u2))) + lm <= thr;
+}
+
+__host__ __device__ constexpr int cf_cut_step(int N) { return (N + 63) / 64; }
+
+__device__ __forceinline__ int cf_cut_scan(const dh::Params& P, double T, double a, double b,
+                                           double delta, int N) {
+    if (!cf_cut_domain(P, T, delta, N)) return N;
+    const float thr = cf_cut_threshold(delta), ba = (float)(b - a);
+    const int st = cf_cut_step(N);
+    for (int j = 0; j < 64; ++j) {
+        const int k = (j + 1) * st;
+        if (k >= N) break;
+        if (cf_cut_passes(P, (float)T, ba, thr, k)) return k;
+    }
+    return N;
+}
+
+__device__ __forceinline__ int cf_cut_wave(const dh::Params& P, double T, double a, double b,
+                                           double delta, int N, int lane) {
+    if (!cf_cut_domain(P, T, delta, N)) return N;           // uniform
+    const int st = cf_cut_step(N);
+    const int k = (lane + 1) * st;
+    const bool ok = k < N && cf_cut_passes(P, (float)T, (float)(b - a), cf_cut_threshold(delta), k);
+    const unsigned long long m = __ballot(ok);
+    return m ? (__ffsll((long long)m)) * st : N;      // lowest passing lane j: (j + 1) st
+}
+
 // per-table values staged in LDS by the prologue lane of the table:
 //   [0..5] a, b, e^b, e^a, 2/(b-a), pi/(b-a) | [6..21] CfConsts | [22] S0, [23] r, [24] T,
 //   [25] K/S0 below which the clamp test must be evaluated, [26] above which (prefilter),
-//   [27] group's first option, [28] group size (as doubles), [29] the discount e^{-rT}
-constexpr int kTabC = 30;
+//   [27] group's first option, [28] group size (as doubles), [29] the discount e^{-rT},
+//   [30] K_cf: the CF entries k < K_cf are evaluated (cf_cut_scan), as a double
+constexpr int kTabC = 31;
 constexpr double kClampMargin = 1e-9;   // relative safety margin of the K-space prefilter
 static_assert(sizeof(dh::CfConsts) == 16 * sizeof(double), "CfConsts layout");
 
@@ -279,6 +386,7 @@ __device__ __forceinline__ void table_prologue(const PriceArgs& A, int64_t q, do
     c[27] = gr.x;
     c[28] = gr.y;
     c[29] = exp(-P.r * T);
+    c[30] = cf_cut_scan(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N);
 }
 
 // table_prologue run by one wave in lockstep (the fused kernel's wave 0): the two variance
@@ -376,6 +484,7 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const Fu
     CC.half_sj2 = 0.5 * (P.sj * P.sj);
     CC.muj = P.muj;
     CC.lt = P.lam * T;
+    const int kcf = cf_cut_wave(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, lane);
     if (lane == 0) {
         c[0] = a;
         c[1] = b;
@@ -393,6 +502,7 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const Fu
         c[27] = gr.x;
         c[28] = gr.y;
         c[29] = lane_bcast(e, 5);
+        c[30] = kcf;
     }
 }
 
@@ -420,27 +530,6 @@ __global__ __launch_bounds__(kBlock) void table_prologue_kernel(PriceArgs A, int
 #define DH_FUSED_WAVES_WIDE 5   // the one-option-per-lane-group variant for large grids (<= 96 VGPRs)
 #endif
 
-// Adaptive tail of the angle sums.  A table's terms k >= n_eff are not summed, n_eff - 1 being
-// the last k >= 1 with |T2_k| > tail_delta.  Past it |T6_k| = |T2_k| / u_k <= |T2_k| (b - a)/pi,
-// so the dropped part of S is at most (1 + (b - a)/pi) N delta = 2^-72 S0/(b - a), and a price
-// moves by at most e^{-rT} e^{xK} 2^-72 S0/(b - a) = e^{-rT} 2^-72 K/(b - a): below 2^-64 of its
-// own k = 0 term e^{-rT} w0 V0 (w0 = 1/(b - a); V0 >= 0.0048 K because the log-strike lies at
-// least 0.1 inside [a, b] -- clamp-widened options take the per-term path), i.e. far inside the
-// price's rounding.  The characteristic function decays like exp(-c u): at N = 512 (C3) a table
-// keeps ~26% of its terms, at N = 256 ~46%, at N = 128 ~97%.  Every path forms n_eff from the
-// same T2_k values with the same expressions, so fused and split keep their identical bits.
-// NaN / inf entries (and a NaN delta) always count as kept: a NaN still reaches the price.
-constexpr double kTailScale = 0x1.0p-72;
-__device__ __forceinline__ double tail_delta(double scale, double S0, double ba, int N) {
-    return scale * S0 / (ba * (1.0 + ba * (1.0 / dh::kPi)) * (double)N);
-}
-__device__ __forceinline__ int tail_keep(int k, double T2, double delta) {
-    return fabs(T2) <= delta ? 0 : k + 1;
-}
-__device__ __forceinline__ int xor_max_i(int v, int width) {
-    for (int off = 1; off < width; off <<= 1) v = max(v, __shfl_xor(v, off, 64));
-    return v;
-}
 
 // CF entries of one table slot (thread t of TPT): k = t, t + TPT, ..., emitted in increasing k
 // (the k-sums' order) as emit(k, u_k, w_k).
@@ -502,6 +591,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
             const double a = c[0], b = c[1], eb = c[2], ea = c[3], scale = c[4], piba = c[5];
             const double S0 = c[22], T = c[24], lo = c[25], hi = c[26];
             const int g0 = (int)c[27], gn = has ? (int)c[28] : 0;
+            const int kcf = (int)c[30];                  // CF entries k < K_cf (cf_cut_scan)
             double* t2 = t2s + (TPT > 64 ? slot * N : 0);
             double c0 = 0.0, c5 = 0.0, w0 = 0.0;
             const double delta = tail_delta(A.tail, S0, b - a, N);
@@ -514,7 +604,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                 }
                 double* tw = table_w(A, q);
                 const int ts = table_step(A);
-                table_entries<TPT>(CC, t, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
+                table_entries<TPT>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
                     tw[k * ts] = w;
                     if (k == 0) {
                         w0 = 0.5 * w;
@@ -539,7 +629,7 @@ __global__ __launch_bounds__(kBlock, DH_TABLE_WAVES) void cos_table_kernel(Price
                 __syncthreads();
                 if (has && wv == 0) {                          // the canonical 64-lane order
                     w0 = lane == 0 ? w0s[slot] : 0.0;
-                    for (int k = lane; k < N; k += 64) {
+                    for (int k = lane; k < kcf; k += 64) {
                         if (k == 0) continue;
                         const double T2 = t2[k];
                         const double cb = (k & 1) ? -1.0 : 1.0;
@@ -1360,6 +1450,7 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
             const double* c = shc[it];
             const double a = c[0], eb = c[2], ea = c[3], scale = c[4], piba = c[5];
             const double S0 = c[22], T = c[24];
+            const int kcf = (int)c[30];                  // CF entries k < K_cf (cf_cut_scan)
             dh::CfConsts CC;
             {
                 double* cc = (double*)&CC;
@@ -1369,7 +1460,7 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
             const double delta = tail_delta(A.tail, S0, c[1] - a, N);
             double c0 = 0.0, c5 = 0.0, w0 = 0.0;
             int ne = 0;
-            table_entries<TPT>(CC, sub, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
+            table_entries<TPT>(CC, sub, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
                 if (k == 0) {
                     w0 = 0.5 * w;
                     tb[0] = make_double2(0.0, 0.0);
@@ -1636,6 +1727,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
 
     const double a = shc[0], b = shc[1], eb = shc[2], ea = shc[3], scale = shc[4], piba = shc[5];
     const double T = shc[24];
+    const int kcf = (int)shc[30];                    // CF entries k < K_cf (cf_cut_wave)
     // ---- clamp-widened options (double_heston.py:135-137), decided and priced per wave: the
     //      masks first (a short loop), the pricing loop only where a mask is set (rare: its
     //      register traffic stays off the common path).  The masks and prices are read after the
@@ -1696,7 +1788,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP(A, 6);
         DH_STAMP_T(A, 19, 64);
         DH_STAMP_T(A, 20, 192);
-        table_entries<TPT1>(CC, t, N, piba, T, a, scale, sct, [&](int k, double u, double w) {
+        table_entries<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
             L.tu[k] = u;
             if (k == 0) {
                 w0s = 0.5 * w;
@@ -1730,7 +1822,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         const double delta = tail_delta(A.tail, S0, b - a, N);
         double c0 = 0.0, c5 = 0.0;
         int ne = 0;                                  // n_eff (tail_keep), on wave 0 with c0
-        for (int k = lane; k < N; k += 64) {
+        for (int k = lane; k < kcf; k += 64) {
             if (k == 0) continue;
             const double T2 = L.t26[k].x;
             const double cb = (k & 1) ? -1.0 : 1.0;
