@@ -59,6 +59,8 @@ FLOP_TERM = 12
 FLOP_OPT = 110
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector peak (spec)
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+SIMDS = 1024              # 256 CUs x 4 SIMDs
+NS_FP64_WAVE_INST = 2.05  # fully fed v_fma_f64 issue per SIMD, ns per wave-instruction (ubench)
 BYTES_PER_OPTION = 8 + 8 + 1 + 8 + 4   # K, T, is_call, mkt, perm read per (param set, option)
 
 GEN_LO = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
@@ -214,8 +216,18 @@ def pmc_executed(config, ker_ms, launches=1):
     if not fl or any(f is None for f in fl):
         return None
     tf = sum(fl) * launches / (ker_ms * 1e-3) / 1e12
-    return {"exec_fp64_flop_per_request": sum(fl) * launches, "TFLOPs": round(tf, 3),
-            "frac": round(tf / PEAK_FP64_TFLOPS, 4), "source": f"profiles/pmc_traffic.json [{config}]"}
+    out = {"exec_fp64_flop_per_request": sum(fl) * launches, "TFLOPs": round(tf, 3),
+           "frac": round(tf / PEAK_FP64_TFLOPS, 4), "source": f"profiles/pmc_traffic.json [{config}]"}
+    vi = [k.get("valu_insts") for k in ks.values()]
+    if vi and all(v is not None for v in vi):
+        # VALU issue: the request's wave-instructions at the fully fed fp64 rate per SIMD
+        # (tools/ubench/valu_rates.hip) over the SIMDs x request time -- how close the kernels
+        # run to the issue bound that limits them
+        n = sum(vi) * launches
+        out["valu_issue"] = {"valu_wave_insts": n, "ns_per_fp64_wave_inst": NS_FP64_WAVE_INST,
+                             "simds": SIMDS,
+                             "frac": round(n * NS_FP64_WAVE_INST * 1e-9 / (SIMDS * ker_ms * 1e-3), 4)}
+    return out
 
 
 def make_roofline(flop_conv, survey_flop, ker_ms, executed, traffic, alg_bytes, label,
@@ -237,6 +249,7 @@ def make_roofline(flop_conv, survey_flop, ker_ms, executed, traffic, alg_bytes, 
          "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": traffic,
          "flop_basis": basis, "flop_per_launch": flop, "kernel": label,
          "kernel_ms": round(ker_ms, 5),
+         "valu_issue": (executed or {}).get("valu_issue"),
          "convention": {"flop_per_launch": flop_conv, "achieved_TFLOPs": round(conv_tf, 3),
                         "frac": round(conv_tf / PEAK_FP64_TFLOPS, 4),
                         "counts": f"FLOP_TAB {FLOP_TAB} / FLOP_TERM {FLOP_TERM} / FLOP_OPT "
