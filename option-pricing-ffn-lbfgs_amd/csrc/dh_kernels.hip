@@ -270,8 +270,9 @@ __device__ __forceinline__ int xor_max_i(int v, int width) {
 // by the tail cut anyway: the CF is not evaluated there (K_cf, prologue slot 30).  The bound
 // follows |phi| closely: at N = 512 (C3) K_cf is ~7 terms past n_eff, ~28% of N
 // (tests/test_cf_cut_bound.py checks the bound against the oracle's CF).
-// The test runs in fp32 (native-rate transcendentals; its errors, ~1e-6 relative on log values
-// of magnitude < 1e3 near the threshold, sit far inside the 0.01 log-margin it keeps) on the
+// The test runs in fp32 at the native rate (v_exp / v_log / v_sqrt / v_rcp, ~1 ulp each; the
+// errors, ~1e-6 relative on log values of magnitude < 1e3 near the threshold, sit far inside the
+// 0.01 log-margin it keeps) on the
 // candidates k_j = (j + 1) ceil(N / 64), j < 64: K_cf is the first that passes (else N).  The
 // one-lane scan (table_prologue) and the wave's ballot (table_prologue_wave) test the same
 // candidates with the same bits, so they pick the same one.  Series of N < 512 terms are not
@@ -282,15 +283,20 @@ __device__ __forceinline__ int xor_max_i(int v, int width) {
 // (delta < 0) are not cut either.
 constexpr int kCfCutMinN = 512;
 
+// fp32 at the native rate: v_sqrt_f32, v_exp_f32 / v_log_f32 (base 2, ~1 ulp) and v_rcp_f32
+__device__ __forceinline__ float f_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504f); }
+__device__ __forceinline__ float f_log(float x) { return __builtin_amdgcn_logf(x) * 0.693147181f; }
+__device__ __forceinline__ float f_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+
 __device__ __forceinline__ float cir_log_laplace(float s, float tau, float v0, float kap,
                                                  float th, float sig) {
 #pragma clang fp contract(off)
     const float s2 = sig * sig;
-    const float g = sqrtf(kap * kap + 2.0f * s2 * s);
-    const float e = expf(-(g * tau));
+    const float g = __builtin_amdgcn_sqrtf(kap * kap + 2.0f * s2 * s);
+    const float e = f_exp(-(g * tau));
     const float den = (g + kap) * (1.0f - e) + 2.0f * g * e;
-    const float B = 2.0f * s * (1.0f - e) / den;
-    const float A = (2.0f * kap * th / s2) * (logf(2.0f * g) + 0.5f * (kap - g) * tau - logf(den));
+    const float B = f_div(2.0f * s * (1.0f - e), den);
+    const float A = f_div(2.0f * kap * th, s2) * (f_log(2.0f * g) + 0.5f * (kap - g) * tau - f_log(den));
     return A - B * v0;
 }
 
@@ -310,14 +316,14 @@ __device__ __forceinline__ float cf_cut_threshold(double delta) {
 __device__ __forceinline__ bool cf_cut_passes(const dh::Params& P, float T, float ba, float thr,
                                               int k) {
 #pragma clang fp contract(off)
-    const float u = (float)k * (3.14159265f / ba);
+    const float u = (float)k * f_div(3.14159265f, ba);
     const float u2 = u * u;
     const float lm =
         cir_log_laplace(0.5f * u2 * (1.0f - (float)P.r1 * (float)P.r1), T, (float)P.v01,
                         (float)P.k1, (float)P.t1, (float)P.s1) +
         cir_log_laplace(0.5f * u2 * (1.0f - (float)P.r2 * (float)P.r2), T, (float)P.v02,
                         (float)P.k2, (float)P.t2, (float)P.s2);
-    return logf(2.0f * (float)P.S0 / (ba * (1.0f + u2))) + lm <= thr;
+    return f_log(f_div(2.0f * (float)P.S0, ba * (1.0f + u2))) + lm <= thr;
 }
 
 __host__ __device__ constexpr int cf_cut_step(int N) { return (N + 63) / 64; }
@@ -446,26 +452,57 @@ static_assert(offsetof(FusedKargs, A) == kFusedArgsKernargOff, "PriceArgs kernar
 // kernel's entry)
 __device__ const int kLiveOne = 1;
 
-__device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const FusedHead& H,
-                                                    int64_t q, double* c, int lane) {
+// The truncation range of table q (trunc_unclamped's bits) with the two variance factors'
+// cumulants on alternate lanes: table_prologue_wave's first step, and the whole of what
+// prologue_cut_wave needs.
+__device__ __forceinline__ void prologue_range_wave(const PriceArgs& A, const FusedHead& H,
+                                                    int64_t q, int lane, Params& P, double& T,
+                                                    double& a, double& b) {
 #pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
     const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
     const int g = (int)((unsigned)q % (unsigned)H.tpp);
-    const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
-    const double T = H.tsrc[H.paired ? p : g];
-    int2 gr = make_int2((int)p, 1);
-    if (!H.paired) gr = H.groups[g];
+    P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
+    T = H.tsrc[H.paired ? p : g];
     const bool two = lane & 1;                     // factor 2 on odd lanes
     const double v0 = two ? P.v02 : P.v01, k = two ? P.k2 : P.k1, th = two ? P.t2 : P.t1;
     const double sg = two ? P.s2 : P.s1, rh = two ? P.r2 : P.r1;
     double c1j, c2j;
     dh::factor_cumulants(T, P.r, v0, k, th, sg, rh, c1j, c2j);   // double_heston.py:101-118
-    const dh::FactorC Fj = dh::factor_consts(v0, k, th, sg, rh);
     const double c1 = lane_bcast(c1j, 0) + lane_bcast(c1j, 1) + P.lam * T * P.muj;
     const double c2 = lane_bcast(c2j, 0) + lane_bcast(c2j, 1) +
                       P.lam * T * (P.sj * P.sj + P.muj * P.muj);
     const double h = A.L * sqrt(fabs(c2));
-    const double a = c1 - h, b = c1 + h;           // trunc_unclamped (double_heston.py:120-132)
+    a = c1 - h;                                    // trunc_unclamped (double_heston.py:120-132)
+    b = c1 + h;
+}
+
+// K_cf of table q by one wave (cf_cut_wave on prologue_range_wave's range): in the fused kernel
+// a wave other than the prologue's runs it, so the bound's fp32 chain overlaps the prologue's
+// instead of following it.
+__device__ __forceinline__ int prologue_cut_wave(const PriceArgs& A, const FusedHead& H,
+                                                 int64_t q, int lane) {
+    Params P;
+    double T, a, b;
+    prologue_range_wave(A, H, q, lane, P, T, a, b);
+    return cf_cut_wave(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, lane);
+}
+
+// with_cut: also K_cf (slot 30); else the caller's other wave stores it
+__device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const FusedHead& H,
+                                                    int64_t q, double* c, int lane,
+                                                    bool with_cut) {
+#pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
+    Params P;
+    double T, a, b;
+    prologue_range_wave(A, H, q, lane, P, T, a, b);
+    const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
+    const int g = (int)((unsigned)q % (unsigned)H.tpp);
+    int2 gr = make_int2((int)p, 1);
+    if (!H.paired) gr = H.groups[g];
+    const bool two = lane & 1;                     // factor 2 on odd lanes
+    const double v0 = two ? P.v02 : P.v01, k = two ? P.k2 : P.k1, th = two ? P.t2 : P.t1;
+    const double sg = two ? P.s2 : P.s1, rh = two ? P.r2 : P.r1;
+    const dh::FactorC Fj = dh::factor_consts(v0, k, th, sg, rh);
     const int e_lane = lane < 6 ? lane : 0;
     const double arg = e_lane == 0 ? b : e_lane == 1 ? a : e_lane == 2 ? a + 0.1
                      : e_lane == 3 ? b - 0.1 : e_lane == 4 ? P.muj + 0.5 * (P.sj * P.sj)
@@ -484,7 +521,8 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const Fu
     CC.half_sj2 = 0.5 * (P.sj * P.sj);
     CC.muj = P.muj;
     CC.lt = P.lam * T;
-    const int kcf = cf_cut_wave(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, lane);
+    const int kcf =
+        with_cut ? cf_cut_wave(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, lane) : 0;
     if (lane == 0) {
         c[0] = a;
         c[1] = b;
@@ -502,7 +540,7 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const Fu
         c[27] = gr.x;
         c[28] = gr.y;
         c[29] = lane_bcast(e, 5);
-        c[30] = kcf;
+        if (with_cut) c[30] = kcf;
     }
 }
 
@@ -1687,10 +1725,16 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // ---- prologue (wave 0, lane-parallel) || per-option staging (wave 0 takes the last
     //      indices).  The prologue comes first in program order and reads the preloaded
     //      arguments only, so its loads issue before any kernel-argument wait ----
+    // K_cf on the block's last wave (its CF-cut test overlaps wave 0's prologue; the staging loop
+    // below gives that wave option indices nthr - 128 .. nthr - 65, none on C3's 100-option tiles)
+    const int wcut = nthr > 64 ? nthr / 64 - 1 : 0;
     if (H.pre) {
         if (t < kTabC) shc[t] = H.pre[q * kTabC + t];
     } else if (wv == 0) {
-        table_prologue_wave(A, H, q, shc, lane);
+        table_prologue_wave(A, H, q, shc, lane, wcut == 0);
+    } else if (wv == wcut) {
+        const int kcf = A.N < kCfCutMinN ? A.N : prologue_cut_wave(A, H, q, lane);
+        if (lane == 0) shc[30] = kcf;
     }
     DH_STAMP(A, 8);
     const int N = A.N;
