@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import threading
 import time
+from operator import itemgetter
 from dataclasses import dataclass
 from typing import Dict, List
 
@@ -178,7 +179,7 @@ class DoubleHestonJumpCalibrator:
         self.spot = spot
         self.risk_free_rate = risk_free_rate
         self.market_options = market_options
-        self.market_prices = np.array([opt["price"] for opt in market_options])
+        self.market_prices = np.array(list(map(itemgetter("price"), market_options)))
         self.param_names = list(PARAM_NAMES)
         self.n_calls = 0
         self.best_loss = np.inf
@@ -213,14 +214,18 @@ class DoubleHestonJumpCalibrator:
     # ---- device surface -----------------------------------------------------------------
     def _get_surface(self):
         if self._surface_ok is None:
+            opts = self.market_options
             try:
-                flags = [resolve_call(o["option_type"]) for o in self.market_options]
+                # resolve_call once per distinct type string (10,000-option surfaces hold two)
+                types = list(map(itemgetter("option_type"), opts))
+                rule = {t: resolve_call(t) for t in set(types)}
+                flags = list(map(rule.__getitem__, types))
             except Exception:          # '' / non-string option types: the reference returns 1e10
                 self._surface_ok = False
                 return None
             ctx = _native.default_context(self.device)
-            K = [o["strike"] for o in self.market_options]
-            T = [o["maturity"] for o in self.market_options]
+            K = list(map(itemgetter("strike"), opts))
+            T = list(map(itemgetter("maturity"), opts))
             self._surface = _native.Surface(ctx, K, T, flags, self.market_prices)
             self._surface_ok = True
         return self._surface if self._surface_ok else None
