@@ -307,9 +307,10 @@ __device__ __forceinline__ bool cf_cut_domain(const dh::Params& P, double T, dou
            P.lam >= 0.0 && T > 0.0 && P.S0 > 0.0;
 }
 
-// log(delta / 2) less the margin: the candidates' threshold (one double log per table)
+// log(delta / 2) less the margin: the candidates' threshold (fp32, native rate; delta > 0 and
+// far above fp32's normal range: ~2^-80 S0)
 __device__ __forceinline__ float cf_cut_threshold(double delta) {
-    return (float)log(0.5 * delta) - 0.01f;
+    return f_log(0.5f * (float)delta) - 0.01f;
 }
 
 // bound(k) <= delta / 2 with the margin, in logs, fp32
