@@ -275,13 +275,13 @@ __device__ __forceinline__ int xor_max_i(int v, int width) {
 // 0.01 log-margin it keeps) on the
 // candidates k_j = (j + 1) ceil(N / 64), j < 64: K_cf is the first that passes (else N).  The
 // one-lane scan (table_prologue) and the wave's ballot (table_prologue_wave) test the same
-// candidates with the same bits, so they pick the same one.  Series of N < 512 terms are not
-// cut: at N = 128 (C1, C5) almost every term lies inside the bound, and at N = 256 the CF entries
-// are one per thread, so the halved CF work bought nothing while the test lengthened C2's
-// latency-bound prologue (12.1 -> 12.9 us; C4 unchanged).  Parameters outside the model's domain
-// (kappa, sigma, T <= 0, theta, v0, lambda < 0, |rho| > 1, NaN) and a disabled tail cut
-// (delta < 0) are not cut either.
-constexpr int kCfCutMinN = 512;
+// candidates with the same bits, so they pick the same one.  Series of N < 256 terms are not
+// cut: at N = 128 (C1, C5) almost every term lies inside the bound.  At N = 256 (C2, C4) the cut
+// costs C2 nothing now that the test runs on its own wave at the native fp32 rate, and C4 gains
+// 2.5% (with the first, libm-rate test on wave 0 it had cost C2 12.1 -> 12.9 us).  Parameters
+// outside the model's domain (kappa, sigma, T <= 0, theta, v0, lambda < 0, |rho| > 1, NaN) and a
+// disabled tail cut (delta < 0) are not cut either.
+constexpr int kCfCutMinN = 256;
 
 // fp32 at the native rate: v_sqrt_f32, v_exp_f32 / v_log_f32 (base 2, ~1 ulp) and v_rcp_f32
 __device__ __forceinline__ float f_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504f); }
