@@ -579,6 +579,48 @@ def test_tail_cut_moves_prices_below_rounding(dh, N):
         assert rel_close(cut[p], want, FID_RTOL, BAR_ATOL).all(), np.max(np.abs(cut[p] - want))
 
 
+@pytest.mark.parametrize("N", [256, 512, 1024])
+def test_cf_cut_extreme_parameters(dh, N):
+    """The CF cut skips CF entries past a certified bound, tested in fp32 with a
+    log margin.  Stress it where the bound is least comfortable: |rho| near 1 (the Gaussian part
+    (1 - rho^2) I nearly vanishes), large and small vol-of-vol, short and long maturities, jump
+    heavy sets.  With the cuts on, prices stay within 1e-13 K of the uncut kernels and match the
+    oracle at the fidelity bar."""
+    from dhcos import _native
+    rs = np.random.RandomState(77 + N)
+    P = 12
+    params = np.empty((P, 13))
+    for i in range(P):
+        r1, r2 = [(-0.999, 0.999), (0.98, -0.97), (-0.2, 0.0), (0.5, -0.999)][i % 4]
+        s1, s2 = [(0.05, 1.5), (2.0, 0.1), (0.3, 0.3)][i % 3]
+        params[i] = [0.01 + 0.1 * rs.rand(), 0.2 + 5 * rs.rand(), 0.01 + 0.1 * rs.rand(), s1, r1,
+                     0.01 + 0.1 * rs.rand(), 0.2 + 5 * rs.rand(), 0.01 + 0.1 * rs.rand(), s2, r2,
+                     [0.0, 0.5, 3.0][i % 3], -0.3 + 0.4 * rs.rand(), 0.02 + 0.4 * rs.rand()]
+    rec = np.zeros((P, 16))
+    rec[:, :13], rec[:, 13], rec[:, 14] = params, 100.0, 0.03
+    K = 100.0 * rs.uniform(0.85, 1.15, 300)
+    T = rs.choice([0.02, 0.1, 0.5, 2.0, 5.0], 300)
+    call = rs.rand(300) < 0.5
+    ctx = _native.default_context()
+    surf = _native.Surface(ctx, K, T, call)
+    cut = surf.price(rec, N)
+    ctx.set_tail_cut(False)
+    try:
+        full = surf.price(rec, N)
+    finally:
+        ctx.set_tail_cut(True)
+    ok = np.isfinite(full)
+    assert np.array_equal(np.isfinite(cut), ok)
+    d = np.abs(cut - full)[ok]
+    print(f"N={N}: max |cut - full| {d.max():.3e}, changed {np.mean(d > 0):.3f}")
+    assert np.all(d <= 1e-13 * np.broadcast_to(K, cut.shape)[ok]), d.max()
+    for p in range(0, P, 3):
+        want = O.price_many(params[p], 100.0, K, T, 0.03, call, N)
+        good = np.isfinite(want)
+        assert rel_close(cut[p][good], want[good], BAR_RTOL, BAR_ATOL).all(), \
+            np.max(np.abs(cut[p][good] - want[good]))
+
+
 def test_clamped_options_across_mask_words_and_tiles(dh):
     """The table kernel decides and prices clamp-widened options (double_heston.py:135-137) and
     the option kernel looks them up by a per-(p, group) bit mask.  One maturity group of 300
