@@ -667,16 +667,17 @@ def test_clamped_options_across_mask_words_and_tiles(dh):
     assert rel_close(pairs, want[0, far], FID_RTOL, BAR_ATOL).all()
 
 
-@pytest.mark.parametrize("P", [16500, 16503])
-def test_small_tile_path_large_call(dh, P):
+@pytest.mark.parametrize("P,N", [(16500, 128), (16503, 128), (16500, 512)])
+def test_small_tile_path_large_call(dh, P, N):
     """Calls with >= 65,536 tasks on surfaces whose tiles hold <= 16 options (generator grids)
     run the lane-per-option-group kernel.  Its prices must agree with the large-tile kernel
     (the same rows priced in a small call) and with the oracle, including clamp-widened
     strikes, and its loss must be the loss of its own prices.  The split path then stores the
-    tables 16 to a line (kTabTile): 16,503 x 4 tables end in a partial tile."""
+    tables 16 to a line (kTabTile): 16,503 x 4 tables end in a partial tile.  At N = 512 the
+    generator kernel takes 4 tables per block and its prologue lanes run the CF cut's scan."""
     from dhcos import _native
     rs = np.random.RandomState(33)
-    N = 128                                             # P x 4 maturity tiles >= 66,000 tasks
+    # P x 4 maturity tiles >= 66,000 tasks
     Krel = np.concatenate([np.tile(np.linspace(80.0, 120.0, 8), 4), [3.0, 900.0]])
     T = np.concatenate([np.repeat([0.25, 0.5, 1.0, 2.0], 8), [0.25, 0.25]])
     call = np.ones(T.size, dtype=np.int8)

@@ -78,6 +78,17 @@ def test_null_and_range_arguments_are_rejected():
     lib.dh_device_count(C.byref(n))
     assert n.value >= 0
     assert np.int8(1) == 1
+    for setter in (lib.dh_ctx_set_tail_cut, lib.dh_ctx_set_exact, lib.dh_ctx_set_path):
+        assert setter(None, 1) == -1                  # a null context, not a crash
+
+
+def test_gen_assemble_arguments_are_rejected():
+    """dh_gen_assemble (host code) validates its sizes and pointers."""
+    from dhcos import _native
+    lib = _native.load()
+    assert lib.dh_gen_assemble(None, None, None, None, -1, 3, None, None, None) == -1
+    assert lib.dh_gen_assemble(None, None, None, None, 4, 3, None, None, None) == -1
+    assert lib.dh_gen_assemble(None, None, None, None, 0, 3, None, None, None) == 0
 
 
 def test_comm_and_async_fg_arguments_are_rejected():
