@@ -146,8 +146,24 @@ constexpr int kStamps = 24;
             (A).stamps[(size_t)blockIdx.x * kStamps + (i)] = _t;                          \
         }                                                                                  \
     } while (0)
+// the block's residency in the chip-wide 100 MHz clock (s_memrealtime): slot 23 = start << 32 |
+// end, low 32 bits of each (tools/stamps.py --timeline)
+#define DH_RT_BEGIN(A)                                                                     \
+    unsigned long long _rt0 = 0;                                                           \
+    if ((A).stamps && threadIdx.x == 0)                                                    \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt0)::"memory")
+#define DH_RT_END(A)                                                                       \
+    do {                                                                                   \
+        if ((A).stamps && threadIdx.x == 0) {                                              \
+            unsigned long long _rt1;                                                       \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt1)::"memory"); \
+            (A).stamps[(size_t)blockIdx.x * kStamps + 23] = (_rt0 << 32) | (_rt1 & 0xffffffffull); \
+        }                                                                                  \
+    } while (0)
 #else
 #define DH_STAMP_T(A, i, thr) do {} while (0)
+#define DH_RT_BEGIN(A) do {} while (0)
+#define DH_RT_END(A) do {} while (0)
 #endif
 #define DH_STAMP(A, i) DH_STAMP_T(A, i, 0)
 
@@ -568,6 +584,19 @@ __global__ __launch_bounds__(kBlock) void table_prologue_kernel(PriceArgs A, int
 #ifndef DH_FUSED_WAVES_WIDE
 #define DH_FUSED_WAVES_WIDE 5   // the one-option-per-lane-group variant for large grids (<= 96 VGPRs)
 #endif
+#ifndef DH_PRIO
+#define DH_PRIO 1
+#endif
+// Wave priority on a block's serial phases (the prologue, the k-sums, the loss hand-off): the
+// waves the rest of the block waits for at a barrier issue ahead of the other resident blocks'
+// waves on their SIMD, whose CF and option sums fill the slots they leave.  Scheduling only:
+// the same instructions, so the same bits.
+__device__ __forceinline__ void serial_prio(bool on) {
+    if constexpr (DH_PRIO > 0) {
+        if (on) __builtin_amdgcn_s_setprio(DH_PRIO);
+        else __builtin_amdgcn_s_setprio(0);
+    }
+}
 
 
 // CF entries of one table slot (thread t of TPT): k = t, t + TPT, ..., emitted in increasing k
@@ -1482,8 +1511,10 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
     const int io = t / TPT, oo = (t % TPT) / S, jj = t % S;   // option phase: table, option, k-block
     for (int64_t b0 = (int64_t)blockIdx.x * TB; b0 < n_q; b0 += (int64_t)gridDim.x * TB) {
         const int nb = (int)min<int64_t>(TB, n_q - b0);
+        if (t < 64) serial_prio(true);               // the prologue lanes' wave
         if (t < nb) table_prologue(A, b0 + t, shc[t]);
         __syncthreads();
+        serial_prio(false);
         // ---- CF entries of table slot `it` into LDS ----
         if (it < nb) {
             const double* c = shc[it];
@@ -1650,6 +1681,7 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
         if (A.part_sse) {
             __syncthreads();
             // one lane per table: the options' terms in option order, then the hand-off
+            if (t < 64) serial_prio(true);
             if (t < nb) {
                 const double* cc = shc[t];
                 const int ng = (int)cc[28];
@@ -1721,6 +1753,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const int64_t q = blockIdx.x;
     const int64_t p = (int64_t)(blockIdx.x / (unsigned)H.tpp);    // 32-bit: grids < 2^31 blocks
     const int g = (int)(blockIdx.x % (unsigned)H.tpp);
+    DH_RT_BEGIN(A);
     DH_STAMP(A, 0);
 
     // ---- prologue (wave 0, lane-parallel) || per-option staging (wave 0 takes the last
@@ -1729,6 +1762,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // K_cf on the block's last wave (its CF-cut test overlaps wave 0's prologue; the staging loop
     // below gives that wave option indices nthr - 128 .. nthr - 65, none on C3's 100-option tiles)
     const int wcut = nthr > 64 ? nthr / 64 - 1 : 0;
+    if (!H.pre && (wv == 0 || wv == wcut)) serial_prio(true);
     if (H.pre) {
         if (t < kTabC) shc[t] = H.pre[q * kTabC + t];
     } else if (wv == 0) {
@@ -1767,6 +1801,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         L.exK[i] = ratio;
     }
     __syncthreads();
+    serial_prio(false);
     if (__builtin_amdgcn_readfirstlane(live_v) <= 0) return;   // every block reads the same count
     DH_STAMP(A, 1);
 
@@ -1863,6 +1898,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // 5-wave build keeps both on wave 0: its register allocation cost C4 2%)
     const int w5 = (WV <= DH_FUSED_WAVES && nthr >= 192) ? nthr / 64 - 1 : 0;
     if (wv == 0 || wv == w5) {
+        serial_prio(true);
         const bool f0 = wv == 0, f5 = wv == w5;
         const double delta = tail_delta(A.tail, S0, b - a, N);
         double c0 = 0.0, c5 = 0.0;
@@ -1905,6 +1941,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         }
     }
     __syncthreads();
+    serial_prio(false);
     DH_STAMP(A, 3);
 
     const Consts C{0.0 + red[0][0], 0.0 + red[1][0], 0.0 + red[2][0], 0.0 + red[3][0], a, b, eb, ea};
@@ -1912,9 +1949,13 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     DH_STAMP(A, 4);
     if (A.part_sse) {
         __syncthreads();
-        if (t < 64) task_loss(A, p, A.paired ? p : p * A.n_tiles + g, gn, t, L.sse, L.bad);
+        if (t < 64) {
+            serial_prio(true);
+            task_loss(A, p, A.paired ? p : p * A.n_tiles + g, gn, t, L.sse, L.bad);
+        }
     }
     DH_STAMP(A, 5);
+    DH_RT_END(A);
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--dev", action="store_true",
                     help="params / outputs in device memory (loss_dev), as the bench and the "
                          "device L-BFGS driver run; default: the host API (zero-copy params)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="fused kernel: the blocks' residency (slot 23, s_memrealtime, 100 MHz) "
+                         "as resident-block counts over the launch")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     opts, S0, r = bench.make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
@@ -85,6 +88,8 @@ def main():
         for nm, i0, i1 in detail:
             c = st[:, i1] - st[:, i0]
             print(f"    {nm:20s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}")
+        if args.timeline:
+            timeline(st[:, 23])
         return
     tb = st[st[:, 4] > 0]
     print(f"{args.config} {args.mode}: table-kernel blocks {len(tb)}")
@@ -100,6 +105,29 @@ def main():
               f"max {c.max():8.0f} cycles")
     life = st[:, 3] - st[:, 0]
     print(f"  lifetime median {np.median(life):8.0f}  max {life.max():8.0f}")
+
+
+def timeline(rt):
+    """Resident fused blocks over the launch from the 100 MHz start/end stamps (10 ns ticks)."""
+    t0 = (rt >> 32).astype(np.int64)
+    t1 = (rt & 0xffffffff).astype(np.int64)
+    t1 = np.where(t1 < t0, t1 + (1 << 32), t1)
+    base = t0.min()
+    t0, t1 = t0 - base, t1 - base
+    span = t1.max()
+    print(f"  timeline: {len(t0)} blocks over {span * 0.01:.2f} us; last start at "
+          f"{t0.max() * 0.01:.2f} us; block residency median {np.median(t1 - t0) * 0.01:.2f} us "
+          f"(p10 {np.percentile(t1 - t0, 10) * 0.01:.2f}, max {(t1 - t0).max() * 0.01:.2f})")
+    nb = 40
+    edges = np.linspace(0, span, nb + 1)
+    mids = 0.5 * (edges[1:] + edges[:-1])
+    res = [int(np.sum((t0 <= m) & (t1 > m))) for m in mids]
+    peak = max(res)
+    for m, c in zip(mids, res):
+        print(f"    {m * 0.01:7.2f} us  {c:5d} {'#' * int(60 * c / max(peak, 1))}")
+    # work-conserving estimate: the residency integral at the peak count
+    busy = float(np.sum(t1 - t0))
+    print(f"  resident-block integral / (peak {peak} x span): {busy / (peak * span):.3f}")
 
 
 if __name__ == "__main__":
