@@ -820,13 +820,13 @@ __device__ __forceinline__ double option_sum(const Consts& C, bool is_call, doub
 // entries are read four steps ahead: each step's chain is one FMA deep and no LDS latency sits
 // between steps.
 __device__ __forceinline__ double angle_sum_1(int k1, int G, int N, double dx, double cg,
-                                              double sg, const double* tu, const double2* t26,
+                                              double sg, double piba, const double2* t26,
                                               const double2* sct) {
     double sc = 0.0, ss = 0.0;
     const double c2 = 2.0 * cg;
     for (int k0 = k1; k0 < N; k0 += kAnchor * G) {
         double cx, sx;
-        dh::dsincos_t(tu[k0] * dx, sct, &sx, &cx);
+        dh::dsincos_t(k0 * piba * dx, sct, &sx, &cx);          // u_k0 as the table's u
         double cp = cx * cg + sx * sg;                  // cos((k - G) th)
         double sp = sx * cg - cx * sg;                  // sin((k - G) th)
         const int kend = min(N, k0 + kAnchor * G);
@@ -876,10 +876,10 @@ __device__ __forceinline__ double angle_sum_1(int k1, int G, int N, double dx, d
 template <int RR>
 __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double (&dx)[RR],
                                              const double (&cg)[RR], const double (&sg)[RR],
-                                             const double* tu, const double2* t26,
+                                             double piba, const double2* t26,
                                              const double2* sct, double (&sum)[RR]) {
     if constexpr (RR == 1) {
-        sum[0] = angle_sum_1(k1, G, N, dx[0], cg[0], sg[0], tu, t26, sct);
+        sum[0] = angle_sum_1(k1, G, N, dx[0], cg[0], sg[0], piba, t26, sct);
         return;
     }
 #pragma unroll
@@ -892,7 +892,7 @@ __device__ __forceinline__ void angle_sums_r(int k1, int G, int N, const double 
     // registers instead of being copied, with the table entries read ahead of the arithmetic
     for (int k0 = k1; k0 < N; k0 += kAnchor * G) {
         double cx[RR], sx[RR], cp[RR], sp[RR];
-        const double uk = tu[k0];
+        const double uk = k0 * piba;                 // u_k0, the table's expression
 #pragma unroll
         for (int j = 0; j < RR; ++j) {
             dh::dsincos_t(uk * dx[j], sct, &sx[j], &cx[j]);
@@ -1006,15 +1006,14 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
 }
 
 __host__ __device__ constexpr int option_lds_doubles(int N, int opt_cap) {
-    // (T2,T6)[N] u[N] | K, mkt, sse, bad, xK, e^xK, cos/sin step [opt_cap] |
-    // call, perm [opt_cap] ints, rounded to whole 16-byte pairs
-    return 3 * N + 8 * opt_cap + ((2 * opt_cap + 3) / 4) * 2;
+    // (T2,T6)[N] | K, mkt, sse, bad, xK, e^xK, cos/sin step [opt_cap] | call, perm [opt_cap]
+    // ints, rounded to whole 16-byte pairs (u_k = k pi/(b - a) is re-formed where needed)
+    return 2 * N + 8 * opt_cap + ((2 * opt_cap + 3) / 4) * 2;
 }
 
 // LDS view of one staged tile: the expanded (p, g) table and the per-option arrays
 struct TileLds {
     double2* t26;     // (T2_k, T6_k)
-    double* tu;
     double* K;
     double* mkt;
     double* sse;
@@ -1030,8 +1029,7 @@ struct TileLds {
 __device__ __forceinline__ TileLds tile_lds(double* base, int N, int cap) {
     TileLds L;
     L.t26 = (double2*)base;
-    L.tu = base + 2 * N;
-    L.K = base + 3 * N;
+    L.K = base + 2 * N;
     L.mkt = L.K + cap;
     L.sse = L.mkt + cap;
     L.bad = L.sse + cap;
@@ -1100,7 +1098,7 @@ __device__ __forceinline__ void tile_sums_r(const PriceArgs& A, int64_t p, const
         }
         double sm[RT];
         if (pass == 0) DH_STAMP(A, 9);
-        angle_sums_r<RT>(1 + gl, G, Ne, dx, cs, ss, L.tu, L.t26, sct, sm);
+        angle_sums_r<RT>(1 + gl, G, Ne, dx, cs, ss, dh::kPi / (C.b - C.a), L.t26, sct, sm);
         if (pass == 0) DH_STAMP(A, 10);
         if (lds_red) {
             if (gvalid) {
@@ -1186,7 +1184,6 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
     __shared__ double2 sct[dh::kMathTab];
     dh::load_sincos_table(sct);                                // synchronised by the staging barrier
     double2* t26 = L.t26;
-    double* tu = L.tu;
     double* lK = L.K;
     double* lmkt = L.mkt;
     double* lsse = L.sse;
@@ -1235,7 +1232,6 @@ __global__ __launch_bounds__(kBlock, DH_OPTION_WAVES) void cos_option_kernel(Pri
             const double u = k * piba;
             const double T2 = k == 0 ? 0.0 : w * P.S0 * dh::drcp(1.0 + u * u);
             t26[k] = make_double2(T2, k == 0 ? 0.0 : -(T2 * dh::drcp(u)));
-            tu[k] = u;
         }
         const double ustep = G * dh::kPi / ba;
         const int g0 = A.paired ? (int)p : A.groups[g].x;
@@ -1761,7 +1757,10 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     //      arguments only, so its loads issue before any kernel-argument wait ----
     // K_cf on the block's last wave (its CF-cut test overlaps wave 0's prologue; the staging loop
     // below gives that wave option indices nthr - 128 .. nthr - 65, none on C3's 100-option tiles)
-    const int wcut = nthr > 64 ? nthr / 64 - 1 : 0;
+#ifndef DH_CUT_W0
+#define DH_CUT_W0 0
+#endif
+    const int wcut = (nthr > 64 && !DH_CUT_W0) ? nthr / 64 - 1 : 0;
     if (!H.pre && (wv == 0 || wv == wcut)) serial_prio(true);
     if (H.pre) {
         if (t < kTabC) shc[t] = H.pre[q * kTabC + t];
@@ -1869,7 +1868,6 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP_T(A, 19, 64);
         DH_STAMP_T(A, 20, 192);
         table_entries<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
-            L.tu[k] = u;
             if (k == 0) {
                 w0s = 0.5 * w;
                 L.t26[0] = make_double2(0.0, 0.0);

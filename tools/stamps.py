@@ -90,6 +90,16 @@ def main():
             print(f"    {nm:20s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}")
         if args.timeline:
             timeline(st[:, 23])
+            life = st[:, 5] - st[:, 0]
+            ng = surf.n_groups if hasattr(surf, "n_groups") else cfg["nT"]
+            g = np.arange(len(st)) % ng
+            print(f"  lifetime (cycles) by maturity group ({ng} groups, group 0 = shortest T):")
+            for lo in range(0, ng, max(1, ng // 10)):
+                sel = (g >= lo) & (g < lo + max(1, ng // 10))
+                print(f"    groups {lo:3d}..: median {np.median(life[sel]):8.0f}  "
+                      f"p90 {np.percentile(life[sel], 90):8.0f}  "
+                      f"cf {np.median(st[sel, 2] - st[sel, 1]):7.0f}  "
+                      f"sums {np.median(st[sel, 4] - st[sel, 3]):7.0f}")
         return
     tb = st[st[:, 4] > 0]
     print(f"{args.config} {args.mode}: table-kernel blocks {len(tb)}")
