@@ -136,7 +136,7 @@ __device__ __forceinline__ bool halted(const PriceArgs& A) {
 
 // In-kernel phase stamps, compiled only into the diagnostic build (make stamps): lane 0 of each
 // block of the option kernel writes s_memtime at its phase boundaries.
-constexpr int kStamps = 24;
+constexpr int kStamps = 32;     // [24, 28): HW_ID of waves 0..3 (SIMD placement)
 #ifdef DH_STAMPS
 #define DH_STAMP_T(A, i, thr)                                                              \
     do {                                                                                   \
@@ -151,7 +151,12 @@ constexpr int kStamps = 24;
 #define DH_RT_BEGIN(A)                                                                     \
     unsigned long long _rt0 = 0;                                                           \
     if ((A).stamps && threadIdx.x == 0)                                                    \
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt0)::"memory")
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt0)::"memory");    \
+    if ((A).stamps && (threadIdx.x & 63) == 0 && threadIdx.x < 256) {                      \
+        unsigned _hw;                                                                      \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(_hw));                  \
+        (A).stamps[(size_t)blockIdx.x * kStamps + 24 + (threadIdx.x >> 6)] = _hw;          \
+    }
 #define DH_RT_END(A)                                                                       \
     do {                                                                                   \
         if ((A).stamps && threadIdx.x == 0) {                                              \
@@ -1792,10 +1797,9 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     //      arguments only, so its loads issue before any kernel-argument wait ----
     // K_cf on the block's last wave (its CF-cut test overlaps wave 0's prologue; the staging loop
     // below gives that wave option indices nthr - 128 .. nthr - 65, none on C3's 100-option tiles)
-#ifndef DH_CUT_W0
-#define DH_CUT_W0 0
-#endif
-    const int wcut = (nthr > 64 && !DH_CUT_W0) ? nthr / 64 - 1 : 0;
+    // (the <= 96-VGPR wide build runs it on wave 0 after the prologue: one range computation
+    // less, and the build's register allocation gains: C4 -2.6%)
+    const int wcut = (nthr > 64 && WV <= DH_FUSED_WAVES) ? nthr / 64 - 1 : 0;
     if (!H.pre && (wv == 0 || wv == wcut)) serial_prio(true);
     if (H.pre) {
         if (t < kTabC) shc[t] = H.pre[q * kTabC + t];

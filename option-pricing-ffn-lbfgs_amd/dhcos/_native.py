@@ -27,7 +27,7 @@ MAX_N_PER_TERM = 65536         # longest accepted; longer than MAX_N runs the pe
 STRIKE_ABSOLUTE = 0
 STRIKE_PCT_SPOT = 1
 PATH_AUTO, PATH_SPLIT, PATH_FUSED, PATH_GEN = 0, 1, 2, 3   # PATH_GEN: reported only (AUTO)
-STAMPS_PER_BLOCK = 24          # kStamps of the DH_STAMPS build (csrc/dh_kernels.hip)
+STAMPS_PER_BLOCK = 32          # kStamps of the DH_STAMPS build (csrc/dh_kernels.hip)
 
 _dp = C.POINTER(C.c_double)
 _i8p = C.POINTER(C.c_int8)

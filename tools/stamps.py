@@ -90,6 +90,14 @@ def main():
             print(f"    {nm:20s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}")
         if args.timeline:
             timeline(st[:, 23])
+            hw = st[:, 24:28].astype(np.int64)
+            simd = (hw >> 4) & 3
+            cu = (hw >> 8) & 15
+            print("  SIMD of wave w (HW_ID bits 5:4), share of blocks per SIMD 0..3:")
+            for w in range(4):
+                sh = [np.mean(simd[:, w] == k) for k in range(4)]
+                print(f"    wave {w}: " + "  ".join(f"{x:.2f}" for x in sh))
+            print(f"  waves of a block on one CU: {np.mean((cu == cu[:, :1]).all(axis=1)):.3f}")
             life = st[:, 5] - st[:, 0]
             ng = surf.n_groups if hasattr(surf, "n_groups") else cfg["nT"]
             g = np.arange(len(st)) % ng
