@@ -229,6 +229,15 @@ int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* c
                 int64_t n_samples, const double* lo, const double* hi, int n_opt, double alpha,
                 double spot0, double ret_mu, double ret_sigma, double noise_sigma, double* params,
                 double* spots, double* noise);
+/* dh_gen_draw that also publishes its progress: *done (required) is stored, with release order,
+ * as the count of leading samples whose params, spot and noise rows are complete (after every
+ * chunk of 65,536 samples, and n_samples at the end), so a caller thread can price finished rows
+ * while the draw runs.  Same draws, same bits, same final RNG state as dh_gen_draw.           */
+int dh_gen_draw_progress(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,
+                         double* cached_gauss, int64_t n_samples, const double* lo,
+                         const double* hi, int n_opt, double alpha, double spot0, double ret_mu,
+                         double ret_sigma, double noise_sigma, double* params, double* spots,
+                         double* noise, int64_t* done);
 /* The generator's host arithmetic after pricing (synthetic_generator.py:141-157), per sample i
  * and option j of [n_samples][n_opt] row-major arrays: market = model + noise * model, loss[i] =
  * mean_j ((model - market) / market)^2 formed as np.mean forms it (bit for bit), strikes =

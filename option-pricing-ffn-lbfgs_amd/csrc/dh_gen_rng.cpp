@@ -274,11 +274,17 @@ constexpr int64_t kSplitMin = 4096;
 
 }  // namespace
 
-extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,
-                           double* cached_gauss, int64_t n_samples, const double* lo,
-                           const double* hi, int n_opt, double alpha, double spot0,
-                           double ret_mu, double ret_sigma, double noise_sigma, double* params,
-                           double* spots, double* noise) {
+namespace {
+
+// done (optional): the count of leading samples whose params, spot and noise are written, stored
+// with release order after each chunk (a concurrent reader may consume those rows)
+int gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* cached_gauss,
+             int64_t n_samples, const double* lo, const double* hi, int n_opt, double alpha,
+             double spot0, double ret_mu, double ret_sigma, double noise_sigma, double* params,
+             double* spots, double* noise, int64_t* done) {
+    auto publish = [done](int64_t v) {
+        if (done) __atomic_store_n(done, v, __ATOMIC_RELEASE);
+    };
     if (!mt_key || !mt_pos || !has_gauss || !cached_gauss || !lo || !hi) return DH_E_ARG;
     if (n_samples < 0 || n_opt < 0) return DH_E_ARG;
     if (n_samples > 0 && (!params || !spots || (n_opt > 0 && !noise))) return DH_E_ARG;
@@ -375,6 +381,7 @@ extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss
                     if (!sl.full) return;
                 }
                 consume(sl);
+                publish(sl.c1);                             // rows < c1 complete
                 {
                     std::lock_guard<std::mutex> l(mu);
                     sl.full = false;
@@ -439,7 +446,29 @@ extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss
     *mt_pos = g.pos;
     *has_gauss = g.has_gauss;
     *cached_gauss = g.gauss;
+    publish(n_samples);
     return DH_OK;
+}
+
+}  // namespace
+
+extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,
+                           double* cached_gauss, int64_t n_samples, const double* lo,
+                           const double* hi, int n_opt, double alpha, double spot0,
+                           double ret_mu, double ret_sigma, double noise_sigma, double* params,
+                           double* spots, double* noise) {
+    return gen_draw(mt_key, mt_pos, has_gauss, cached_gauss, n_samples, lo, hi, n_opt, alpha,
+                    spot0, ret_mu, ret_sigma, noise_sigma, params, spots, noise, nullptr);
+}
+
+extern "C" int dh_gen_draw_progress(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,
+                                    double* cached_gauss, int64_t n_samples, const double* lo,
+                                    const double* hi, int n_opt, double alpha, double spot0,
+                                    double ret_mu, double ret_sigma, double noise_sigma,
+                                    double* params, double* spots, double* noise, int64_t* done) {
+    if (!done) return DH_E_ARG;
+    return gen_draw(mt_key, mt_pos, has_gauss, cached_gauss, n_samples, lo, hi, n_opt, alpha,
+                    spot0, ret_mu, ret_sigma, noise_sigma, params, spots, noise, done);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -82,6 +82,10 @@ SIGNATURES = {
     "dh_gen_draw": (C.c_int, [C.POINTER(C.c_uint32), _i32p, _i32p, _dp, C.c_int64, _dp, _dp,
                               C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                               _dp, _dp, _dp]),
+    "dh_gen_draw_progress": (C.c_int, [C.POINTER(C.c_uint32), _i32p, _i32p, _dp, C.c_int64, _dp,
+                                       _dp, C.c_int, C.c_double, C.c_double, C.c_double,
+                                       C.c_double, C.c_double, _dp, _dp, _dp,
+                                       C.POINTER(C.c_int64)]),
     "dh_gen_assemble": (C.c_int, [_dp, _dp, _dp, _dp, C.c_int64, C.c_int, _dp, _dp, _dp]),
     "dh_price_batch": (C.c_int, [_vp, _dp, C.c_int64, _dp, _dp, _i8p, C.c_int, C.c_int,
                                  C.c_double, _dp]),
@@ -576,6 +580,60 @@ def gen_draw(n_samples, lo, hi, n_opt, alpha, spot0, ret_mu, ret_sigma, noise_si
                               _ptr(noise)))
     np.random.set_state((name, key, c_pos.value, c_has.value, c_cached.value))
     return params, spots, noise
+
+
+class GenDraw:
+    """dh_gen_draw_progress on a worker thread (the ctypes call releases the GIL): the same
+    draws as gen_draw, whose finished rows the caller may consume while the rest are drawn.
+    ``ready(e)`` blocks until rows < e of params / spots / noise are complete; ``finish()``
+    joins the draw, leaves np.random's state where gen_draw leaves it and returns
+    (params, spots, noise).  np.random must not be used between the two."""
+
+    def __init__(self, n_samples, lo, hi, n_opt, alpha, spot0, ret_mu, ret_sigma, noise_sigma):
+        st = np.random.get_state()
+        if st[0] != "MT19937":
+            raise NativeError(f"unsupported bit generator {st[0]}")
+        self._name = st[0]
+        self._key = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
+        self._pos, self._has = C.c_int32(int(st[2])), C.c_int32(int(st[3]))
+        self._cached = C.c_double(st[4])
+        n = self.n = int(n_samples)
+        self.params, self.spots = np.empty((n, 13)), np.empty(n)
+        self.noise = np.empty((n, int(n_opt)))
+        self._lo, self._hi = _f64(lo), _f64(hi)
+        self._args = (int(n_opt), float(alpha), float(spot0), float(ret_mu), float(ret_sigma),
+                      float(noise_sigma))
+        self._done = C.c_int64(0)
+        self._rc = None
+        self._finished = False
+        lib = load()
+        self._thread = threading.Thread(target=self._run, args=(lib,), daemon=True)
+        self._thread.start()
+
+    def _run(self, lib):
+        n_opt, alpha, spot0, ret_mu, ret_sigma, noise_sigma = self._args
+        self._rc = lib.dh_gen_draw_progress(
+            self._key.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(self._pos),
+            C.byref(self._has), C.byref(self._cached), self.n, _ptr(self._lo), _ptr(self._hi),
+            n_opt, alpha, spot0, ret_mu, ret_sigma, noise_sigma, _ptr(self.params),
+            _ptr(self.spots), _ptr(self.noise), C.byref(self._done))
+
+    def ready(self, e):
+        e = min(int(e), self.n)
+        while self._done.value < e and self._thread.is_alive():
+            self._thread.join(5e-5)
+        if self._done.value < e:                      # the draw ended early: its error
+            self.finish()
+            raise NativeError("dh_gen_draw_progress stopped before the requested rows")
+
+    def finish(self):
+        if not self._finished:
+            self._thread.join()
+            self._finished = True
+            _check(self._rc if self._rc is not None else -1)   # None: the thread raised
+            np.random.set_state((self._name, self._key, self._pos.value, self._has.value,
+                                 self._cached.value))
+        return self.params, self.spots, self.noise
 
 
 def gen_assemble(model, noise, spots, k_rel):

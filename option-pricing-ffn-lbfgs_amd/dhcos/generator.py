@@ -91,6 +91,15 @@ def draw_paths(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
     return _native.gen_draw(n_samples, lo, hi, n_opt, ALPHA, SPOT_BASE, 0.0003, 0.01, 0.02)
 
 
+def draw_paths_async(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
+    """draw_paths on a worker thread (_native.GenDraw): its rows can be consumed as they are
+    finished (``ready(e)``); ``finish()`` returns what draw_paths returns."""
+    lo = np.array([v[0] for v in PARAM_RANGES.values()])
+    hi = np.array([v[1] for v in PARAM_RANGES.values()])
+    n_opt = len(strikes) * len(maturities)
+    return _native.GenDraw(n_samples, lo, hi, n_opt, ALPHA, SPOT_BASE, 0.0003, 0.01, 0.02)
+
+
 def draw_paths_numpy(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
     """draw_paths as a per-sample NumPy loop (the reference's calls, vectorised per sample);
     kept as the tests' cross-check of the native draw."""
@@ -115,8 +124,10 @@ def draw_paths_numpy(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
 
 
 def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES, r=RISK_FREE,
-               chunk=1 << 18, device=None):
-    """GPU: price every sample's call grid (T outer, K inner -- the reference's loop order)."""
+               chunk=1 << 18, device=None, ready=None):
+    """GPU: price every sample's call grid (T outer, K inner -- the reference's loop order).
+    ``ready(e)``, if given, is called before rows [s, e) are read (a draw still in progress,
+    _native.GenDraw); the chunks, and so the launches and the bits, are the same either way."""
     ctx = _native.default_context(device)
     Krel = np.tile(np.asarray(strikes, dtype=np.float64), len(maturities))
     T = np.repeat(np.asarray(maturities, dtype=np.float64), len(strikes))
@@ -126,6 +137,8 @@ def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES,
     out = np.empty((n, T.size))
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
+        if ready is not None:
+            ready(e)
         rec = np.empty((e - s, _native.PARAM_STRIDE))
         rec[:, :13] = params[s:e]
         rec[:, 13] = spots[s:e]
@@ -140,9 +153,14 @@ def generate_synthetic_calibrations(n_samples: int = 500,
                                     save_path: str = "lbfgs_calibrations_synthetic.pkl", *,
                                     N: int = 128, device=None, as_arrays: bool = False,
                                     verbose: bool = True):
-    """Generate ``n_samples`` synthetic calibrations (synthetic_generator.py:25-234)."""
-    params, spots, noise = draw_paths(n_samples)
-    model = price_grid(params, spots, N=N, device=device)
+    """Generate ``n_samples`` synthetic calibrations (synthetic_generator.py:25-234).  The native
+    draw runs on a worker thread and the GPU prices each chunk of samples as soon as the draw has
+    finished it (the draw dominates a 1M-sample run, profiles/r03_generator_e2e.json)."""
+    d = draw_paths_async(n_samples)
+    try:
+        model = price_grid(d.params, d.spots, N=N, device=device, ready=d.ready)
+    finally:
+        params, spots, noise = d.finish()
     return assemble(params, spots, noise, model, save_path, as_arrays=as_arrays,
                     verbose=verbose, N=N)
 

@@ -58,6 +58,48 @@ def test_native_draw_rejects_bad_arguments():
     assert lib.dh_gen_draw(*args) == -1          # negative sample count
 
 
+@pytest.mark.parametrize("seed,n,pre", [(0, 0, 0), (7, 1, 1), (5, 4096, 0), (11, 140000, 1)])
+def test_progress_draw_equals_draw(seed, n, pre):
+    """dh_gen_draw_progress on its worker thread (_native.GenDraw, what
+    generate_synthetic_calibrations overlaps with the GPU pricing): the same rows, the same
+    continuation of np.random, and rows published only once complete (read at each ready())."""
+    np.random.seed(seed)
+    for _ in range(pre):
+        np.random.normal()
+    want = G.draw_paths(n)
+    after_want = np.random.random(7)
+    np.random.seed(seed)
+    for _ in range(pre):
+        np.random.normal()
+    d = G.draw_paths_async(n)
+    for e in range(0, n + 1, 65536):
+        d.ready(e)                                   # rows < e final from here on
+        assert np.array_equal(d.params[:e], want[0][:e]) and np.array_equal(d.spots[:e], want[1][:e])
+        assert np.array_equal(d.noise[:e], want[2][:e])
+    got = d.finish()
+    after_got = np.random.random(7)
+    for a, b in zip(got, want):
+        assert a.shape == b.shape and np.array_equal(a, b)
+    assert np.array_equal(after_got, after_want)
+
+
+def test_progress_draw_requires_counter():
+    import ctypes as C
+    from dhcos import _native
+    lib = _native.load()
+    np.random.seed(0)
+    key = np.ascontiguousarray(np.random.get_state()[1], dtype=np.uint32)
+    pos, hg, cg = C.c_int32(624), C.c_int32(0), C.c_double(0.0)
+    lo, hi = np.zeros(13), np.ones(13)
+    out = [np.empty((2, 13)), np.empty(2), np.empty((2, 15))]
+    args = [key.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(pos), C.byref(hg), C.byref(cg), 2,
+            _native._ptr(lo), _native._ptr(hi), 15, 0.9, 100.0, 0.0, 0.01, 0.02] + \
+        [_native._ptr(a) for a in out]
+    assert lib.dh_gen_draw_progress(*args, None) == -1        # no progress counter
+    done = C.c_int64(0)
+    assert lib.dh_gen_draw_progress(*args, C.byref(done)) == 0 and done.value == 2
+
+
 def test_trading_dates_match_reference_loop():
     """synthetic_generator.py:59-67's weekend-skipping loop, restated here as the check."""
     from datetime import datetime, timedelta

@@ -40,9 +40,20 @@ def main():
         if rep:                                   # rep 0 is the warm-up
             for k, v in zip(stages, (t1 - t0, t2 - t1, t3 - t2, t3 - t0)):
                 stages[k].append(v)
+    # the API call itself: the draw on a worker thread, each pricing chunk as soon as it is drawn
+    pipe = []
+    for rep in range(a.reps + 1):
+        np.random.seed(0)
+        t0 = time.perf_counter()
+        G.generate_synthetic_calibrations(a.n, None, as_arrays=True, verbose=False)
+        if rep:
+            pipe.append(time.perf_counter() - t0)
     out = {k: float(np.median(v)) for k, v in stages.items()}
+    out["generate_synthetic_calibrations"] = float(np.median(pipe))
     out.update(samples=a.n, options_per_sample=15, reps=a.reps, cpu=platform.processor() or None,
-               call="draw_paths + price_grid (host API, N=128) + assemble(as_arrays=True)")
+               call="draw_paths + price_grid (host API, N=128) + assemble(as_arrays=True), one "
+                    "after the other; generate_synthetic_calibrations(n, as_arrays=True): the "
+                    "API, draw and pricing overlapped")
     try:
         with open("/proc/cpuinfo") as fh:
             out["cpu"] = next(l.split(":", 1)[1].strip() for l in fh if l.startswith("model name"))
