@@ -530,6 +530,16 @@ def main():
     torch.cuda.synchronize()
     sse_h, bad_h, _ = surf.loss_terms(host[K_], N)
     assert np.array_equal(sse_h, d_sse[K_].cpu().numpy()), "device/host path mismatch"
+    # host-API rate (PCIe-inclusive: params H2D, losses D2H, synchronous) -- reported, not
+    # `value`.  Measured ahead of the warm-up: a few ms of requests that also bring the GPU from
+    # the idle of the CPU-baseline leg to its sustained clock before the W warm-up steps
+    prices_per_step = S * M
+    n_host = max(5, min(K_, 50))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n_host):
+        surf.loss_terms(host[i], N)
+    host_rate = prices_per_step * n_host / (time.perf_counter() - t0)
     for i in range(W_):
         run(K_ + i)
 
@@ -547,16 +557,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    prices_per_step = S * M
     value = prices_per_step * K_ * world / dt
-
-    # host-API rate (PCIe-inclusive: params H2D, losses D2H, synchronous) -- reported, not `value`
-    n_host = max(5, min(K_, 50))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(n_host):
-        surf.loss_terms(host[i], N)
-    host_rate = prices_per_step * n_host / (time.perf_counter() - t0)
 
     # ---- roofline of the dominant op: one request = cos_table_kernel + cos_option_kernel ----
     reps = max(20, min(K_, 200))
