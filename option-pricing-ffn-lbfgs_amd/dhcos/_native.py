@@ -636,15 +636,24 @@ class GenDraw:
         return self.params, self.spots, self.noise
 
 
-def gen_assemble(model, noise, spots, k_rel):
+def gen_assemble(model, noise, spots, k_rel, out=None):
     """dh_gen_assemble: the generator's market prices, per-sample losses (np.mean's bits) and
-    absolute strikes from [n, m] model prices and noise.  -> (market, loss, strikes)."""
+    absolute strikes from [n, m] model prices and noise.  -> (market, loss, strikes), written into
+    ``out`` (three C-contiguous float64 arrays of those shapes, e.g. row slices) if given."""
     model, noise = _f64(model), _f64(noise)
     spots, k_rel = _f64(spots), _f64(k_rel)
     n, m = model.shape
     if noise.shape != (n, m) or spots.shape != (n,) or k_rel.shape != (m,):
         raise NativeError("gen_assemble: shape mismatch")
-    market, loss, strikes = np.empty((n, m)), np.empty(n), np.empty((n, m))
+    if out is None:
+        market, loss, strikes = np.empty((n, m)), np.empty(n), np.empty((n, m))
+    else:
+        market, loss, strikes = out
+        for a, shp in ((market, (n, m)), (loss, (n,)), (strikes, (n, m))):
+            if (not isinstance(a, np.ndarray) or a.dtype != np.float64 or a.shape != shp
+                    or not a.flags.c_contiguous or not a.flags.writeable):
+                raise NativeError("gen_assemble: out arrays must be writable C-contiguous float64 "
+                                  "of the input shapes")
     _check(load().dh_gen_assemble(_ptr(model), _ptr(noise), _ptr(spots), _ptr(k_rel), n, m,
                                   _ptr(market), _ptr(loss), _ptr(strikes)))
     return market, loss, strikes

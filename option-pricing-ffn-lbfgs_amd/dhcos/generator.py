@@ -23,6 +23,8 @@ from __future__ import annotations
 import pickle
 from datetime import datetime, timedelta
 
+import threading
+
 import numpy as np
 
 from . import _native
@@ -124,10 +126,11 @@ def draw_paths_numpy(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
 
 
 def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES, r=RISK_FREE,
-               chunk=1 << 18, device=None, ready=None):
+               chunk=1 << 18, device=None, ready=None, on_chunk=None):
     """GPU: price every sample's call grid (T outer, K inner -- the reference's loop order).
     ``ready(e)``, if given, is called before rows [s, e) are read (a draw still in progress,
-    _native.GenDraw); the chunks, and so the launches and the bits, are the same either way."""
+    _native.GenDraw); the chunks, and so the launches and the bits, are the same either way.
+    ``on_chunk(s, e, out)``, if given, is called after rows [s, e) of ``out`` are priced."""
     ctx = _native.default_context(device)
     Krel = np.tile(np.asarray(strikes, dtype=np.float64), len(maturities))
     T = np.repeat(np.asarray(maturities, dtype=np.float64), len(strikes))
@@ -145,6 +148,8 @@ def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES,
         rec[:, 14] = r
         rec[:, 15] = 0.0
         out[s:e] = surf.price(rec, N)
+        if on_chunk is not None:
+            on_chunk(s, e, out)
     surf.close()
     return out
 
@@ -157,15 +162,39 @@ def generate_synthetic_calibrations(n_samples: int = 500,
     draw runs on a worker thread and the GPU prices each chunk of samples as soon as the draw has
     finished it (the draw dominates a 1M-sample run, profiles/r03_generator_e2e.json)."""
     d = draw_paths_async(n_samples)
+    n_opt = d.noise.shape[1]
+    Krel = np.tile(STRIKES_PCT, len(MATURITIES))
+    asm = (np.empty((n_samples, n_opt)), np.empty(n_samples), np.empty((n_samples, n_opt)))
+    workers, errors = [], []
+
+    def assemble_rows(s, e, model):
+        # dh_gen_assemble of the priced rows on a worker thread (the ctypes call releases the
+        # GIL) while the next chunk is drawn and priced; row-wise, so the same bits
+        def work():
+            try:
+                _native.gen_assemble(model[s:e], d.noise[s:e], d.spots[s:e], Krel,
+                                     tuple(a[s:e] for a in asm))
+            except BaseException as exc:          # re-raised by the caller after the join
+                errors.append(exc)
+        t = threading.Thread(target=work)
+        t.start()
+        workers.append(t)
+
     try:
-        model = price_grid(d.params, d.spots, N=N, device=device, ready=d.ready)
+        model = price_grid(d.params, d.spots, N=N, device=device, ready=d.ready,
+                           on_chunk=assemble_rows)
     finally:
         params, spots, noise = d.finish()
+        for t in workers:
+            t.join()
+    if errors:
+        raise errors[0]
     return assemble(params, spots, noise, model, save_path, as_arrays=as_arrays,
-                    verbose=verbose, N=N)
+                    verbose=verbose, N=N, assembled=asm)
 
 
-def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose=True, N=128):
+def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose=True, N=128,
+             assembled=None):
     """Host part after pricing: noise, per-sample loss, output records (:141-183)."""
     say = print if verbose else (lambda *a, **k: None)
     n_samples = params.shape[0]
@@ -182,7 +211,10 @@ def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose
     # market = model + noise * model (:141-142), loss = mean(((model - market)/market)^2)
     # (:154-157) and the absolute strikes in one native pass, NumPy's bits
     # (_native.gen_assemble: dh_gen_assemble)
-    market, losses, strikes = _native.gen_assemble(model, noise, spots, Krel)
+    if assembled is None:
+        market, losses, strikes = _native.gen_assemble(model, noise, spots, Krel)
+    else:                                # formed chunk by chunk during the pricing
+        market, losses, strikes = assembled
     if as_arrays:
         result = dict(dates=dates, spot=spots, risk_free=RISK_FREE, params=params,
                       param_names=names, market_prices=market, model_prices=model,

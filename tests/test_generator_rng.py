@@ -100,6 +100,27 @@ def test_progress_draw_requires_counter():
     assert lib.dh_gen_draw_progress(*args, C.byref(done)) == 0 and done.value == 2
 
 
+def test_gen_assemble_into_row_slices():
+    """gen_assemble(out=...) on row chunks (generate_synthetic_calibrations assembles each
+    priced chunk while the next is drawn and priced) == one call on all rows, bit for bit."""
+    from dhcos import _native
+    rs = np.random.RandomState(4)
+    n, m = 1000, 15
+    model = rs.rand(n, m) + 0.5
+    noise = rs.normal(0, 0.02, (n, m))
+    spots = 100 + rs.rand(n)
+    k = np.tile(np.array([90.0, 95, 100, 105, 110]), 3)
+    want = _native.gen_assemble(model, noise, spots, k)
+    got = (np.empty((n, m)), np.empty(n), np.empty((n, m)))
+    for s in range(0, n, 300):
+        e = min(n, s + 300)
+        _native.gen_assemble(model[s:e], noise[s:e], spots[s:e], k, tuple(a[s:e] for a in got))
+    for a, b in zip(got, want):
+        assert np.array_equal(a, b)
+    with pytest.raises(_native.NativeError):
+        _native.gen_assemble(model, noise, spots, k, (got[0][:, :3], got[1], got[2]))
+
+
 def test_trading_dates_match_reference_loop():
     """synthetic_generator.py:59-67's weekend-skipping loop, restated here as the check."""
     from datetime import datetime, timedelta

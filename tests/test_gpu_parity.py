@@ -513,6 +513,27 @@ def test_generator_matches_reference(dh, gen_golden, tmp_path):
         assert rel_close(r.final_loss, w["final_loss"], 1e-6, 0)
 
 
+def test_generator_pipeline_equals_stages(dh):
+    """generate_synthetic_calibrations overlaps the native draw, the GPU pricing and the
+    assembly chunk by chunk (dh_gen_draw_progress, price_grid's ready / on_chunk): at 300,000
+    samples (two pricing chunks, five draw chunks) every output array equals the stages run one
+    after the other, bit for bit, and np.random continues identically."""
+    from dhcos import generator as G
+    n = 300_000
+    np.random.seed(17)
+    p, s, nz = G.draw_paths(n)
+    model = G.price_grid(p, s)
+    want = G.assemble(p, s, nz, model, None, as_arrays=True, verbose=False)
+    after_want = np.random.random(5)
+    np.random.seed(17)
+    got = G.generate_synthetic_calibrations(n, None, as_arrays=True, verbose=False)
+    after_got = np.random.random(5)
+    for k, v in want.items():
+        if isinstance(v, np.ndarray):
+            assert np.array_equal(got[k], v), k
+    assert np.array_equal(after_got, after_want)
+
+
 def test_loss_handoff_stress(dh):
     """The fused loss reduction (last-arriver hand-off between workgroups, no fences) checked word
     for word against sums formed on the host from the same kernel's prices, over 300 back-to-back
