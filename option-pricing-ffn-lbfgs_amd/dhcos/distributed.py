@@ -228,6 +228,10 @@ def generate_sharded(n_samples: int = 500,
     from . import generator as G
 
     rank, world = _world(group, comm)
+    if world == 1 and comm is None and price_fn is None:
+        # one rank: the single-process API itself (draw, pricing and assembly overlapped)
+        return G.generate_synthetic_calibrations(n_samples, save_path, N=N, device=device,
+                                                 as_arrays=as_arrays, verbose=verbose)
     price_fn = price_fn or (lambda p, s: G.price_grid(p, s, N=N, device=device))
     n_opt = len(G.STRIKES_PCT) * len(G.MATURITIES)
     width = 13 + 1 + n_opt
