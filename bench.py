@@ -26,6 +26,8 @@ sample on rank 0, anchored to the reference by profiles/cpu_anchor.json).
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -61,7 +63,11 @@ PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector peak (spec)
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SIMDS = 1024              # 256 CUs x 4 SIMDs
 NS_FP64_WAVE_INST = 2.05  # fully fed v_fma_f64 issue per SIMD, ns per wave-instruction (ubench)
-BYTES_PER_OPTION = 8 + 8 + 1 + 8 + 4   # K, T, is_call, mkt, perm read per (param set, option)
+# SURVEY 8(d) algorithmic bytes: per option K, T, market price 8 B each + type 1 B, read once per
+# launch; per param set 13 x 8 B in; out 8 B per price (pricing / generator) or per set (loss)
+BYTES_8D_OPTION = 25
+BYTES_8D_SET = 104
+BYTES_8D_OUT = 8
 
 GEN_LO = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
 GEN_HI = np.array([0.08, 4.5, 0.065, 0.5, -0.4, 0.07, 1.2, 0.07, 0.35, -0.2, 0.25, -0.01, 0.12])
@@ -230,13 +236,16 @@ def pmc_executed(config, ker_ms, launches=1):
     return out
 
 
-def make_roofline(flop_conv, survey_flop, ker_ms, executed, traffic, alg_bytes, label,
+def make_roofline(flop_conv, survey_flop, t_ms, executed, traffic, alg_bytes, label,
                   **extra):
-    """The roofline object: `frac` is the counter-executed fp64 fraction of the request (the only
-    hardware-anchored figure: the frozen convention charges the round-1 kernels' flops, and
-    SURVEY 8(d)'s per-term trig is replaced here by table + recurrence, so it exceeds 1 on C3);
-    both conventions are reported beside it.  Without a committed counter pass for the config
-    the frozen convention stands in (flop_basis says which)."""
+    """The roofline object over t_ms, one request's time (the smaller of the isolated HIP-event
+    time and the back-to-back step time): `frac` is the counter-executed fp64 fraction of the
+    request (the only hardware-anchored figure: the frozen convention charges the round-1
+    kernels' flops, and SURVEY 8(d)'s per-term trig is replaced here by table + recurrence, so it
+    exceeds 1 on C3); both conventions are reported beside it.  Without a committed counter pass
+    for the config the frozen convention stands in (flop_basis says which).  `hbm` holds SURVEY
+    8(d)'s algorithmic bytes and the counter bytes (`traffic`), each over t_ms."""
+    ker_ms = t_ms
     conv_tf = flop_conv / (ker_ms * 1e-3) / 1e12
     if executed:
         ach, basis = executed["TFLOPs"], ("executed fp64 flops per request (rocprofv3 "
@@ -260,11 +269,26 @@ def make_roofline(flop_conv, survey_flop, ker_ms, executed, traffic, alg_bytes, 
                        "note": "716 flop-eq per CF + 120 per (set, option, k): charges per-term "
                                "trig the kernels replace by table + recurrence (DESIGN.md 4)"},
          "alg_bytes_per_launch": alg_bytes,
-         "hbm": {"achieved_GBs": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 3),
-                 "peak_GBs": PEAK_HBM_GBS,
-                 "frac": alg_bytes / (ker_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}}
+         "hbm": hbm_block(alg_bytes, traffic, ker_ms)}
     r.update(extra)
     return r
+
+
+def hbm_block(alg_bytes, traffic, t_ms):
+    """HBM side of the roofline: SURVEY 8(d)'s algorithmic bytes per launch and the rocprofv3
+    counter bytes (FETCH_SIZE + WRITE_SIZE of the launch, profiles/pmc_traffic.json), each as
+    GB/s over the request time, and their ratio (above 1: bytes the algorithm does not need --
+    the loss hand-off's padded lines, spills, re-reads)."""
+    t = t_ms * 1e-3
+    out = {"alg_bytes_8d": alg_bytes, "alg_GBs": round(alg_bytes / t / 1e9, 3),
+           "counter_bytes": traffic, "peak_GBs": PEAK_HBM_GBS,
+           "counter_GBs": None if traffic is None else round(traffic / t / 1e9, 3),
+           "counter_over_alg": None if traffic is None else round(traffic / alg_bytes, 3),
+           "bytes_basis": "8(d): 25 B per option (K, T, market, type) once per launch + 104 B "
+                          "per param set in + 8 B per output (price, or loss per set)"}
+    out["frac"] = round((traffic if traffic is not None else alg_bytes) / t / 1e9 / PEAK_HBM_GBS,
+                        6)
+    return out
 
 
 CONFIGS = {
@@ -322,11 +346,33 @@ def calib_leg(S0, r, opts, N, n_starts, world, coll, driver, reps=3):
                          "np.random.seed(0)" + (", starts sharded over ranks" if world > 1 else "")}
 
 
-def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
-    """C5: one step = price every (param set, option) of a 1M-sample generator batch
-    (dh_surface_price_dev, strikes K_relative * spot / 100 formed on the device)."""
+def _max_over_ranks(dt, world, coll):
+    """Barrier, then the max of dt over the ranks (the contract's whole-job time)."""
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([dt], dtype=torch.float64, device=coll)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return dt
+
+
+def event_ms(run, stream, reps):
+    """Median HIP-event time (ms) of run(j) on `stream`, one isolated call per event pair."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for j, (e0, e1) in enumerate(evs):
+        e0.record(stream)
+        run(j)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    return float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+
+def gen_batch(P, N, steps, warmup, dev, stream, rank, world=1, coll=None):
+    """C5 timing: one step = price every (param set, option) of a P-sample generator batch
+    (dh_surface_price_dev, strikes K_relative * spot / 100 formed on the device), after a
+    host/device spot check.  -> dict(value, ms_per_step, ker_ms, P, M, N, n_chunks, surf)."""
     sptr = stream.cuda_stream
-    P, N = cfg["P"], cfg["N"]
     Krel = np.tile(np.linspace(80.0, 120.0, 8), 4)
     T = np.repeat([0.25, 0.5, 1.0, 2.0], 8)
     M = T.size
@@ -341,72 +387,73 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
     d_params = torch.from_numpy(host).to(dev)
     d_out = torch.empty((P, M), dtype=torch.float64, device=dev)
 
-    def run():
+    def run(_j=0):
         surf.price_dev(d_params.data_ptr(), P, d_out.data_ptr(), N=N, stream=sptr)
 
     # correctness spot check first, so that the warm-up passes run right ahead of the timed ones
     run()
     torch.cuda.synchronize()
-    chk = np.arange(0, P, P // 64)
+    chk = np.arange(0, P, max(1, P // 64))
     got = d_out[torch.from_numpy(chk).to(dev)].cpu().numpy()
     ref = surf.price(host[chk], N)          # a 64-set call: the large-tile kernel (last bits differ)
     assert np.all(np.abs(got - ref) <= 1e-12 * np.abs(ref) + 1e-12), "device/host path mismatch"
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         run()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         run()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        tt = torch.tensor([dt], dtype=torch.float64, device=coll)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    value = P * M * args.steps * world / dt
-
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(max(3, min(args.steps, 10)))]
-    for e0, e1 in evs:
-        e0.record(stream)
-        run()
-        e1.record(stream)
-    torch.cuda.synchronize()
-    ker_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
-    G = 4
-    flop = P * G * N * FLOP_TAB + P * M * (N - 1) * FLOP_TERM + P * M * FLOP_OPT
-    survey_flop = P * G * N * 716 + P * M * N * 120
-    alg_bytes = P * 16 * 8 + M * 17 + P * M * 8
+    dt = _max_over_ranks(time.perf_counter() - t0, world, coll)
+    ker_ms = event_ms(run, stream, max(3, min(steps, 10)))
     # launches per batch: the split path (--path split) chunks param sets so one chunk's tables
     # stay within 256 MiB (dh_kernels.hip launch_price: per set = groups x (N + 8 consts + clamp
     # words + largest group) doubles), the committed PMC bytes being per launch pair; the
     # default generator kernel (cos_gen_kernel) is one launch
-    per_p = G * (N + 8 + 1 + 8) * 8
+    per_p = 4 * (N + 8 + 1 + 8) * 8
     n_chunks = -(-P // max(1, (256 << 20) // per_p))
     if surf.ctx.last_path == _native.PATH_GEN:      # one fused launch for the whole batch
         n_chunks = 1
-    tr = pmc_traffic(args.config)
-    roofline = make_roofline(flop, survey_flop, ker_ms,
-                             pmc_executed(args.config, ker_ms, n_chunks),
-                             tr * n_chunks if tr else None, alg_bytes,
-                             kernel_label(surf.ctx) + " (all chunks of one batch, HIP events)",
-                             launch_pairs=n_chunks)
+    return {"value": P * M * steps * world / dt, "ms_per_step": dt / steps * 1e3,
+            "ker_ms": ker_ms, "P": P, "M": M, "N": N, "n_chunks": n_chunks, "surf": surf,
+            "steps": steps, "warmup": warmup}
+
+
+def gen_roofline(g, config):
+    """The generator batch's roofline object (over its per-batch time)."""
+    P, M, N, n_chunks = g["P"], g["M"], g["N"], g["n_chunks"]
+    t_ms = min(g["ker_ms"], g["ms_per_step"])
+    G = 4
+    flop = P * G * N * FLOP_TAB + P * M * (N - 1) * FLOP_TERM + P * M * FLOP_OPT
+    survey_flop = P * G * N * 716 + P * M * N * 120
+    alg_bytes = P * BYTES_8D_SET + M * BYTES_8D_OPTION + P * M * BYTES_8D_OUT
+    tr = pmc_traffic(config)
+    return make_roofline(flop, survey_flop, t_ms, pmc_executed(config, t_ms, n_chunks),
+                         tr * n_chunks if tr else None, alg_bytes,
+                         kernel_label(g["surf"].ctx) + " (all chunks of one batch, HIP events)",
+                         launch_pairs=n_chunks, kernel_ms=round(g["ker_ms"], 5))
+
+
+def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
+    """--config c5: the generator batch as the headline line."""
+    g = gen_batch(cfg["P"], cfg["N"], args.steps, args.warmup, dev, stream, rank, world, coll)
+    line = None
     if rank == 0:
-        line = {"metric": "option-prices/sec (COS, generator batch)", "value": value,
+        line = {"metric": "option-prices/sec (COS, generator batch)", "value": g["value"],
                 "unit": "option-prices/s", "n_gpus": world, "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+                "warmup": args.warmup, "ms_per_step": g["ms_per_step"],
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                 "data": "synthetic",
-                "config": {"workload": cfg["workload"], "param_sets": P, "options": M,
-                           "cos_terms": N, "prices_per_step": P * M, "tail_cut": args.tail_cut,
+                "config": {"workload": cfg["workload"], "param_sets": g["P"], "options": g["M"],
+                           "cos_terms": g["N"], "prices_per_step": g["P"] * g["M"],
+                           "tail_cut": args.tail_cut, "world_size_seen": world,
                            "parallelism": f"independent batches per rank x{world}"},
-                "roofline": roofline}
+                "roofline": gen_roofline(g, args.config)}
         if cpu:
             line["cpu_baseline"] = cpu
-            line["speedup_vs_cpu"] = value / cpu["value"]
+            line["speedup_vs_cpu"] = g["value"] / cpu["value"]
     e2e = None if args.no_calib else generator_end_to_end(world, rank, coll)
     if rank == 0:
         if e2e:
@@ -418,8 +465,8 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
 
 def generator_end_to_end(world, rank, coll, n_samples=1_000_000):
     """generate_synthetic_calibrations(n_samples, as_arrays=True) end to end under
-    np.random.seed(0): the reference's RNG draws (native legacy-NumPy stream on rank 0), its 5 x 3
-    call grid priced on the GPUs (sharded at N > 1), noise and per-sample losses."""
+    np.random.seed(0): the reference's RNG draws (native legacy-NumPy stream), its 5 x 3 call
+    grid priced on the GPUs (sharded at N > 1), noise and per-sample losses."""
     from dhcos import generator as G
     from dhcos.distributed import generate_sharded
     if world > 1:
@@ -429,21 +476,157 @@ def generator_end_to_end(world, rank, coll, n_samples=1_000_000):
     out = generate_sharded(n_samples, None, as_arrays=True, verbose=False)
     dt = time.perf_counter() - t0
     t_draw = None
-    if rank == 0:                       # the host-draw share of it (rank 0 draws for all ranks)
+    if rank == 0:                       # the host-draw share of it
         np.random.seed(0)
         t1 = time.perf_counter()
         G.draw_paths(n_samples)
         t_draw = time.perf_counter() - t1
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=coll)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = _max_over_ranks(dt, world, coll)
     if rank != 0:
         return None
     return {"samples": n_samples, "options_per_sample": int(out["model_prices"].shape[1]),
             "seconds": dt, "samples_per_sec": n_samples / dt, "host_draw_seconds": t_draw,
             "call": "generate_synthetic_calibrations(1_000_000, as_arrays=True), np.random.seed(0)"
-                    + (", pricing sharded over ranks" if world > 1 else "")}
+                    + (", sharded over ranks" if world > 1 else "")}
+
+
+def request_bench(cfg, steps, warmup, world, rank, dev, coll, stream, starts_rank=None):
+    """Function+gradient requests on cfg's surface: `steps` timed back to back after `warmup`,
+    each at different param sets (inputs resident in HBM), plus the median isolated request
+    (HIP events) and the PCIe-inclusive host-API rate.  -> dict."""
+    sptr = stream.cuda_stream
+    opts, S0, r = make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
+    M = len(opts)
+    cal = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"])
+    surf = cal._get_surface()
+    if starts_rank is None:
+        starts_rank = cfg["starts"]
+    S = 14 * starts_rank
+    n_rows = steps + max(warmup, 1)
+    host = step_params(cal, n_rows, starts_rank, seed=100 + rank)
+    d_params = torch.from_numpy(host).to(dev)
+    d_sse = torch.empty((n_rows, S), dtype=torch.float64, device=dev)
+    d_bad = torch.empty((n_rows, S), dtype=torch.int32, device=dev)
+    N = cfg["N"]
+    ptrs = [(d_params[i].data_ptr(), d_sse[i].data_ptr(), d_bad[i].data_ptr())
+            for i in range(n_rows)]
+    loss_dev = surf.loss_dev
+
+    def run(i):
+        pp, ps, pb = ptrs[i % n_rows]
+        loss_dev(pp, S, ps, pb, N=N, stream=sptr)
+
+    # correctness spot check of one step against the host API (same kernel, host copies), before
+    # the warm-up so that the warm-up steps run right ahead of the timed ones; the context's
+    # scratch is shared, so the bench stream is drained around it
+    run(steps)
+    torch.cuda.synchronize()
+    sse_h, bad_h, _ = surf.loss_terms(host[steps], N)
+    assert np.array_equal(sse_h, d_sse[steps].cpu().numpy()), "device/host path mismatch"
+    # host-API rate (PCIe-inclusive: params H2D, losses D2H, synchronous) -- reported, not
+    # `value`.  Measured ahead of the warm-up: a few ms of requests that also bring the GPU from
+    # the idle of the CPU-baseline leg to its sustained clock before the W warm-up steps
+    prices_per_step = S * M
+    n_host = max(5, min(steps, 50))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n_host):
+        surf.loss_terms(host[i % n_rows], N)
+    host_rate = prices_per_step * n_host / (time.perf_counter() - t0)
+
+    def timed(k):
+        for i in range(warmup):
+            run(steps + i)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(k):
+            run(i)
+        torch.cuda.synchronize()
+        return _max_over_ranks(time.perf_counter() - t0, world, coll)
+
+    dt = timed(steps)
+    ker_ms = event_ms(run, stream, max(20, min(steps, 200)))
+    return {"value": prices_per_step * steps * world / dt, "dt": dt,
+            "ms_per_step": dt / steps * 1e3, "ker_ms": ker_ms, "S": S, "M": M, "N": N,
+            "prices_per_step": prices_per_step, "opts": opts, "S0": S0, "r": r, "surf": surf,
+            "host_rate": host_rate, "timed": timed, "run": run, "steps": steps,
+            "groups": len({o["maturity"] for o in opts}), "n_tiles": surf.n_tiles}
+
+
+def request_roofline(q, config):
+    """The request's roofline object (over the smaller of its isolated and back-to-back time)."""
+    S, M, N, groups, n_tiles = q["S"], q["M"], q["N"], q["groups"], q["n_tiles"]
+    t_ms = min(q["ker_ms"], q["ms_per_step"])
+    flop = S * groups * N * FLOP_TAB + S * M * (N - 1) * FLOP_TERM + S * M * FLOP_OPT
+    alg_bytes = M * BYTES_8D_OPTION + S * BYTES_8D_SET + S * BYTES_8D_OUT
+    survey_flop = S * groups * N * 716 + S * M * N * 120        # SURVEY 8(d) convention
+    return make_roofline(flop, survey_flop, t_ms, pmc_executed(config, t_ms),
+                         pmc_traffic(config), alg_bytes,
+                         kernel_label(q["surf"].ctx) + " (one request, HIP events)",
+                         kernel_ms=round(q["ker_ms"], 5),
+                         time_basis="min(kernel_ms, ms_per_step): "
+                                    + ("ms_per_step" if q["ms_per_step"] < q["ker_ms"]
+                                       else "kernel_ms"))
+
+
+def tail_cut_off_leg(q, steps=50):
+    """The same requests with the adaptive tail / certified CF cut off (dh_ctx_set_tail_cut(0):
+    every COS term k < N summed), to show what the cut buys."""
+    ctx = q["surf"].ctx
+    ctx.set_tail_cut(False)
+    try:
+        steps = min(steps, q["steps"])
+        dt = q["timed"](steps)
+        ker = event_ms(q["run"], torch.cuda.current_stream(), 20)
+    finally:
+        ctx.set_tail_cut(True)
+    ms = dt / steps * 1e3
+    return {"ms_per_step": ms, "kernel_ms": ker, "prices_per_sec": q["prices_per_step"] / (ms * 1e-3),
+            "steps": steps, "cut_on_ms_per_step": q["ms_per_step"],
+            "speedup_from_cut": ms / q["ms_per_step"],
+            "note": "same requests, dh_ctx_set_tail_cut(0): every term k < N summed; prices "
+                    "agree with the cut ones to <= 1e-13 K (tests/test_gpu_parity.py)"}
+
+
+def c2_single_start_leg(world, rank, dev, coll, stream, no_calib=False):
+    """configs[1] as stated: the 1,024-option N = 256 surface, its single-start request
+    (14 param sets) and calibrate(300, 1) on both drivers."""
+    cfg = CONFIGS["c2"]
+    q = request_bench(cfg, 100, 20, world, rank, dev, coll, stream, starts_rank=1)
+    out = {"workload": cfg["workload"], "ms_per_request": q["ms_per_step"],
+           "kernel_ms": q["ker_ms"], "prices_per_sec": q["value"],
+           "prices_per_request": q["prices_per_step"], "steps": q["steps"],
+           "roofline_frac": request_roofline(q, "c2")["frac"]}
+    if not no_calib:
+        for drv in ("scipy", "device"):
+            out[f"calibrate_1_start_{drv}"] = calib_leg(q["S0"], q["r"], q["opts"], cfg["N"], 1,
+                                                        world, coll, drv)
+    return out
+
+
+def c5_leg(dev, stream, rank):
+    """The metric's own N = 128: the generator batch (1M param sets x 32 options)."""
+    cfg = CONFIGS["c5"]
+    g = gen_batch(cfg["P"], cfg["N"], 5, 2, dev, stream, rank)
+    rf = gen_roofline(g, "c5")
+    return {"workload": cfg["workload"], "prices_per_sec": g["value"],
+            "ms_per_batch": g["ms_per_step"], "kernel_ms": g["ker_ms"], "steps": 5,
+            "roofline_frac": rf["frac"], "hbm": rf["hbm"]}
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: run N ranks under torch.distributed.run as child
+    processes (never exec: nothing here has touched the GPU, and the parent only waits); rank
+    0's JSON line reaches this process's stdout.  -> the launcher's exit status."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 def main():
@@ -454,6 +637,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-calib", action="store_true", help="skip the full-calibration leg")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the N = 1 side legs of the c3 line (tail cut off, C2 single "
+                         "start, C5 generator batch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--path", default="auto", choices=["auto", "split", "fused"],
                     help="request kernels (libdhcos dh_ctx_set_path): auto, table+option "
@@ -468,9 +654,17 @@ def main():
                     help="CPU-baseline processes (default min(16, os.cpu_count()))")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
 
+    # --gpus N launches its own N ranks when no launcher did (first, before anything touches
+    # the GPU); under a launcher the world must be the one asked for
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     # CPU baseline first, on rank 0 at N = 1 only, before anything initialises the GPU (its
     # process pool forks)
     cpu = None
@@ -478,7 +672,18 @@ def main():
         c_opts, c_S0, c_r = cpu_options(cfg)
         cpu = cpu_baseline(c_opts, c_S0, c_r, cfg["N"], args.cpu_budget, args.cpu_cores)
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(1, torch.cuda.device_count())     # == LOCAL_RANK on a full node
+    n_dev = torch.cuda.device_count()
+    if args.backend == "nccl":
+        # one rank per GPU: RCCL refuses two ranks on one device, and a rank must never fall
+        # back to a shared one silently
+        if n_dev < world or local >= n_dev:
+            sys.exit(f"bench.py: --gpus {world} needs {world} visible GPUs (rank {rank}, "
+                     f"LOCAL_RANK {local}, {n_dev} visible); --backend gloo rehearses several "
+                     "ranks on one GPU")
+    else:
+        if n_dev < 1:
+            sys.exit("bench.py: no GPU visible")
+        local = local % n_dev                # gloo rehearsal: ranks may share a GPU
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -487,6 +692,16 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     coll = dev if args.backend == "nccl" else torch.device("cpu")   # collective tensors
+    world_seen = dist.get_world_size() if world > 1 else 1
+    if world_seen != world:
+        sys.exit(f"bench.py: process group has {world_seen} ranks, expected {world}")
+    if world > 1:                        # every rank on its own device under RCCL
+        t = torch.tensor([local], dtype=torch.int64, device=coll)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        devs = [int(p.item()) for p in parts]
+        if args.backend == "nccl" and len(set(devs)) != world:
+            sys.exit(f"bench.py: ranks share GPUs under RCCL: {devs}")
     os.environ["DHCOS_DEVICE"] = str(local)
     _native.default_context().set_path({"auto": _native.PATH_AUTO, "split": _native.PATH_SPLIT,
                                         "fused": _native.PATH_FUSED}[args.path])
@@ -494,119 +709,61 @@ def main():
     # a dedicated (non-null) stream: libdhcos launches on it and the HIP events time it
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
-    assert sptr, "expected a non-default HIP stream"
+    assert stream.cuda_stream, "expected a non-default HIP stream"
     if cfg.get("gen"):
         return bench_generator(args, cfg, world, rank, dev, coll, stream, cpu)
 
-    opts, S0, r = make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
-    M = len(opts)
-    cal = DoubleHestonJumpCalibrator(S0, r, opts, N=cfg["N"])
-    surf = cal._get_surface()
     # c4 deals its 64 starts over the ranks (strong scaling); the others run a fixed request per
     # rank (weak scaling)
     starts_rank = -(-cfg["starts"] // world) if cfg.get("strong") else cfg["starts"]
-    S = 14 * starts_rank
-    K_, W_ = args.steps, args.warmup
-    n_rows = K_ + max(W_, 1)
-    host = step_params(cal, n_rows, starts_rank, seed=100 + rank)
-    d_params = torch.from_numpy(host).to(dev)
-    d_sse = torch.empty((n_rows, S), dtype=torch.float64, device=dev)
-    d_bad = torch.empty((n_rows, S), dtype=torch.int32, device=dev)
-    N = cfg["N"]
+    q = request_bench(cfg, args.steps, args.warmup, world, rank, dev, coll, stream, starts_rank)
+    roofline = request_roofline(q, args.config)
+    opts, S0, r, N, M = q["opts"], q["S0"], q["r"], q["N"], q["M"]
 
-    ptrs = [(d_params[i].data_ptr(), d_sse[i].data_ptr(), d_bad[i].data_ptr())
-            for i in range(n_rows)]
-    loss_dev = surf.loss_dev
-
-    def run(i):
-        pp, ps, pb = ptrs[i]
-        loss_dev(pp, S, ps, pb, N=N, stream=sptr)
-
-    # correctness spot check of one step against the host API (same kernel, host copies), before
-    # the warm-up so that the warm-up steps run right ahead of the timed ones; the context's
-    # scratch is shared, so the bench stream is drained around it
-    run(K_)
-    torch.cuda.synchronize()
-    sse_h, bad_h, _ = surf.loss_terms(host[K_], N)
-    assert np.array_equal(sse_h, d_sse[K_].cpu().numpy()), "device/host path mismatch"
-    # host-API rate (PCIe-inclusive: params H2D, losses D2H, synchronous) -- reported, not
-    # `value`.  Measured ahead of the warm-up: a few ms of requests that also bring the GPU from
-    # the idle of the CPU-baseline leg to its sustained clock before the W warm-up steps
-    prices_per_step = S * M
-    n_host = max(5, min(K_, 50))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(n_host):
-        surf.loss_terms(host[i], N)
-    host_rate = prices_per_step * n_host / (time.perf_counter() - t0)
-    for i in range(W_):
-        run(K_ + i)
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(K_):
-        run(i)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        tt = torch.tensor([dt], dtype=torch.float64, device=coll)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-
-    value = prices_per_step * K_ * world / dt
-
-    # ---- roofline of the dominant op: one request = cos_table_kernel + cos_option_kernel ----
-    reps = max(20, min(K_, 200))
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(reps)]
-    for j, (e0, e1) in enumerate(evs):
-        e0.record(stream)
-        run(j % K_)
-        e1.record(stream)
-    torch.cuda.synchronize()
-    ker_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
-    n_tiles = surf.n_tiles
-    groups = len({o["maturity"] for o in opts})
-    flop = S * groups * N * FLOP_TAB + S * M * (N - 1) * FLOP_TERM + S * M * FLOP_OPT
-    alg_bytes = S * 16 * 8 + S * M * BYTES_PER_OPTION + S * n_tiles * 12 + S * 12
-    survey_flop = S * groups * N * 716 + S * M * N * 120        # SURVEY 8(d) convention
-    roofline = make_roofline(flop, survey_flop, ker_ms, pmc_executed(args.config, ker_ms),
-                             pmc_traffic(args.config), alg_bytes,
-                             kernel_label(surf.ctx) + " (one request, HIP events)")
+    # side legs (N = 1, the default c3 line): what the cuts buy, configs[1] as stated (single
+    # start), and the metric's own N = 128 (the generator batch)
+    side = {}
+    if world == 1 and args.config == "c3" and not args.no_side:
+        if args.tail_cut == "on":
+            side["tail_cut_off"] = tail_cut_off_leg(q)
+        side["c2_single_start"] = c2_single_start_leg(world, rank, dev, coll, stream,
+                                                      args.no_calib)
+        side["c5_generator_n128"] = c5_leg(dev, stream, rank)
 
     # ---- calibrations/sec: one full calibration of the same surface; at N > 1 its starts are
-    # sharded over the ranks (dhcos.distributed; 3 starts per GPU, weak scaling; c4: 64 starts
-    # in all, strong scaling).  Two optimizer drivers: SciPy's setulb on the host (the reference's
-    # optimizer bit for bit, one launch + one host round trip per lockstep request) and the
-    # device-resident L-BFGS-B (dh_calibrate_lbfgs) ----
+    # sharded over the ranks (dhcos.distributed; the config's starts per GPU, weak scaling; c4:
+    # 64 starts in all, strong scaling).  Two optimizer drivers: SciPy's setulb on the host (the
+    # reference's optimizer bit for bit, one launch + one host round trip per lockstep request)
+    # and the device-resident L-BFGS-B (dh_calibrate_lbfgs) ----
     calib = calib_dev = None
     if not args.no_calib:
-        n_starts = cfg["starts"] if cfg.get("strong") else 3 * world
+        n_starts = cfg["starts"] if cfg.get("strong") else cfg["starts"] * world
         calib = calib_leg(S0, r, opts, N, n_starts, world, coll, "scipy")
         calib_dev = calib_leg(S0, r, opts, N, n_starts, world, coll, "device")
 
     if rank == 0:
         line = {
             "metric": "option-prices/sec (COS, calibration objective) + calibrations/sec",
-            "value": value, "unit": "option-prices/s", "n_gpus": world, "steps": K_,
-            "warmup": W_, "ms_per_step": dt / K_ * 1e3, "higher_is_better": True,
-            "scaling": "strong" if cfg.get("strong") else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "value": q["value"], "unit": "option-prices/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": q["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "strong" if cfg.get("strong") else "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic",
             "config": {"workload": cfg["workload"], "options": M, "cos_terms": N,
-                       "tail_cut": args.tail_cut, "param_sets_per_step": S, "prices_per_step": prices_per_step,
+                       "tail_cut": args.tail_cut, "param_sets_per_step": q["S"],
+                       "prices_per_step": q["prices_per_step"], "world_size_seen": world_seen,
+                       "backend": args.backend if world > 1 else None,
                        "parallelism": f"independent requests per rank x{world}"},
             "roofline": roofline,
-            "host_api_prices_per_sec": host_rate,
+            "host_api_prices_per_sec": q["host_rate"],
         }
+        line.update(side)
         if calib:
             line["calibration"] = calib
             line["calibration_device"] = calib_dev
         if cpu:
             line["cpu_baseline"] = cpu
-            line["speedup_vs_cpu"] = value / cpu["value"]
+            line["speedup_vs_cpu"] = q["value"] / cpu["value"]
             if calib and world == 1:
                 # the same calibration on the CPU port: every loss evaluation prices M options
                 for c in (calib, calib_dev):

@@ -309,15 +309,64 @@ __device__ __forceinline__ float f_exp(float x) { return __builtin_amdgcn_exp2f(
 __device__ __forceinline__ float f_log(float x) { return __builtin_amdgcn_logf(x) * 0.693147181f; }
 __device__ __forceinline__ float f_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 
+// log E[exp(-s I)] of one CIR factor, A(s) - B(s) v0, in a cancellation-free form.  The textbook
+// A = (2 kappa theta / sigma^2) [log(2g) + (kappa - g) tau / 2 - log(den)] takes a difference of
+// O(1) logs and scales it by 2 kappa theta / sigma^2: at small sigma the fp32 rounding of the logs
+// is amplified past the test's margin.  With x = g tau, om = 1 - e^-x,
+// h(x) = x - om >= 0, g - kappa = 2 sigma^2 s / (g + kappa) and den = 2g - (g - kappa) om:
+//   A = -(2 kappa theta s / (g + kappa)) (h - om (R - 1)) / g,
+//   R = -log(1 - y) / y,  y = sigma^2 s om / ((g + kappa) g) <= 1/2,
+// where h and om come from one series for x < 1 (no 1 - e^-x cancellation) and R - 1 from its
+// series for small y.  Each piece is within a few fp32 ulps, h - om (R - 1) cancels by at most a
+// factor of 2 (om (R - 1) <= h / 2), and A, -B v0 are both <= 0: the log-bound is within ~1e-5
+// relative of the exact one for every sigma > 0 (tests/test_cf_cut_bound.py, sigma down to 1e-6,
+// kappa theta / sigma^2 up to 1e9).
 __device__ __forceinline__ float cir_log_laplace(float s, float tau, float v0, float kap,
                                                  float th, float sig) {
 #pragma clang fp contract(off)
     const float s2 = sig * sig;
     const float g = __builtin_amdgcn_sqrtf(kap * kap + 2.0f * s2 * s);
-    const float e = f_exp(-(g * tau));
-    const float den = (g + kap) * (1.0f - e) + 2.0f * g * e;
-    const float B = f_div(2.0f * s * (1.0f - e), den);
-    const float A = f_div(2.0f * kap * th, s2) * (f_log(2.0f * g) + 0.5f * (kap - g) * tau - f_log(den));
+    const float gk = g + kap;
+    const float x = g * tau;
+    float h, om, e;
+    if (x < 1.0f) {          // h = x^2/2 - x^3/6 + ... (Horner through x^11 / 11!: < 1e-8 rel.)
+        float p = 1.0f / 39916800.0f;
+        p = p * -x + 1.0f / 3628800.0f;
+        p = p * -x + 1.0f / 362880.0f;
+        p = p * -x + 1.0f / 40320.0f;
+        p = p * -x + 1.0f / 5040.0f;
+        p = p * -x + 1.0f / 720.0f;
+        p = p * -x + 1.0f / 120.0f;
+        p = p * -x + 1.0f / 24.0f;
+        p = p * -x + 1.0f / 6.0f;
+        p = p * -x + 0.5f;
+        h = p * (x * x);
+        om = x - h;
+        e = 1.0f - om;
+    } else {
+        e = f_exp(-x);
+        om = 1.0f - e;
+        h = x - om;
+    }
+    const float y = f_div(s2 * s * om, gk * g);
+    float rm1;               // R - 1 = y/2 + y^2/3 + y^3/4 + ...
+    if (y < 0.125f) {
+        float q = 1.0f / 9.0f;
+        q = q * y + 1.0f / 8.0f;
+        q = q * y + 1.0f / 7.0f;
+        q = q * y + 1.0f / 6.0f;
+        q = q * y + 1.0f / 5.0f;
+        q = q * y + 0.25f;
+        q = q * y + 1.0f / 3.0f;
+        q = q * y + 0.5f;
+        rm1 = q * y;
+    } else {
+        rm1 = f_div(-f_log(1.0f - y) - y, y);
+    }
+    const float D = f_div(h - om * rm1, g);
+    const float A = -f_div(2.0f * kap * th * s, gk) * D;
+    const float den = gk * om + 2.0f * g * e;
+    const float B = f_div(2.0f * s * om, den);
     return A - B * v0;
 }
 

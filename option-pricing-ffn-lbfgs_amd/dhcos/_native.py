@@ -664,11 +664,11 @@ _tls = threading.local()
 
 def resolve_device(device: int | None = None) -> int:
     """The GPU a call without an explicit ``device=`` runs on, in this order: $DHCOS_DEVICE;
-    under torch.distributed (one process per GPU, e.g. torchrun) torch's current device when
-    torch sees a GPU -- the device the rank bound with ``torch.cuda.set_device`` / the process
-    group's ``device_id``, whatever rank-to-GPU map the caller used -- else $LOCAL_RANK modulo the
-    visible devices; otherwise 0.  ``distributed._comm_device`` puts the collectives' tensors on
-    the same GPU."""
+    under torch.distributed (one process per GPU, e.g. torchrun) the device the rank bound --
+    the process group's ``device_id``, else torch's current device when ``torch.cuda.set_device``
+    moved it off the default 0 -- then $LOCAL_RANK modulo the visible devices (a gloo job that
+    never binds a device: each rank its own GPU, not all on GPU 0); otherwise 0.
+    ``distributed._comm_device`` puts the collectives' tensors on the same GPU."""
     if device is not None:
         return int(device)
     env = os.environ.get("DHCOS_DEVICE")
@@ -678,7 +678,15 @@ def resolve_device(device: int | None = None) -> int:
     dist = getattr(torch, "distributed", None) if torch is not None else None
     if dist is not None and dist.is_available() and dist.is_initialized():
         if torch.cuda.is_available():
-            return int(torch.cuda.current_device())
+            try:
+                bound = dist.distributed_c10d._get_default_group().bound_device_id
+            except Exception:          # noqa: BLE001 -- an older torch without the attribute
+                bound = None
+            if bound is not None and bound.type == "cuda" and bound.index is not None:
+                return int(bound.index)
+            cur = int(torch.cuda.current_device())
+            if cur != 0:
+                return cur
         local = os.environ.get("LOCAL_RANK")
         if local not in (None, ""):
             n = device_count()

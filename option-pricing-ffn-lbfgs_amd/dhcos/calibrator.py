@@ -136,22 +136,52 @@ def _custom_loss(cal):
             or cls.loss_batch is not DoubleHestonJumpCalibrator.loss_batch)
 
 
+class _StartRaised(Exception):
+    """fg_from_losses' compute_loss path: start ``j`` of the group raised; ``rows`` holds the
+    [j, 14] losses of the starts before it (each point evaluated once, as the reference's
+    per-start minimize calls would)."""
+
+    def __init__(self, j, rows):
+        super().__init__(j)
+        self.j, self.rows = j, rows
+
+
+def _fg_rows(F, dx):
+    """(f0, g, low) of [S, 14] losses: SciPy's forward difference and the smallest valid loss
+    (NaN never wins, 1e10 is not valid)."""
+    G = (F[:, 1:] - F[:, :1]) / dx
+    low = np.min(np.where((F == INVALID_LOSS) | np.isnan(F), np.inf, F), axis=1)
+    return F[:, 0].copy(), G, low
+
+
 def fg_from_losses(cal, X0):
     """fg_batch through the calibrator's own losses (``compute_loss`` per point when a subclass
     replaces it, else ``loss_batch``): the 14 points of each request, their losses, SciPy's
-    forward difference and the smallest valid loss (NaN never wins, 1e10 is not valid)."""
+    forward difference and the smallest valid loss.  With a ``compute_loss`` override the starts
+    are evaluated one after another and a start that raises ends the call with ``_StartRaised``
+    (the losses of the starts before it attached), so no point is ever evaluated twice."""
     S = X0.shape[0]
     X, dx = fd_request_points_many(X0)
     custom = getattr(type(cal), "compute_loss", DoubleHestonJumpCalibrator.compute_loss)
     if custom is not DoubleHestonJumpCalibrator.compute_loss and hasattr(cal, "market_options"):
         n0 = cal.n_calls
-        F = np.array([cal.compute_loss(x) for x in X], dtype=np.float64).reshape(S, N_PARAMS + 1)
-        cal.n_calls = n0                # run_starts keeps the per-start counts
+        rows = []
+        try:
+            for j in range(S):
+                pts = X[j * (N_PARAMS + 1):(j + 1) * (N_PARAMS + 1)]
+                try:
+                    rows.append([cal.compute_loss(x) for x in pts])
+                except _native.NativeError:
+                    raise
+                except Exception as exc:      # noqa: BLE001 -- the reference drops this start
+                    raise _StartRaised(j, np.array(rows, dtype=np.float64).reshape(
+                        len(rows), N_PARAMS + 1)) from exc
+        finally:
+            cal.n_calls = n0            # run_starts keeps the per-start counts
+        F = np.array(rows, dtype=np.float64).reshape(S, N_PARAMS + 1)
     else:
         F = cal.loss_batch(X, track=False).reshape(S, N_PARAMS + 1)
-    G = (F[:, 1:] - F[:, :1]) / dx
-    low = np.min(np.where((F == INVALID_LOSS) | np.isnan(F), np.inf, F), axis=1)
-    return F[:, 0].copy(), G, low
+    return _fg_rows(F, dx)
 
 
 def fd_request_points_many(X0, h=FD_ABS_STEP):
@@ -535,21 +565,49 @@ def _fg(cal, X0):
     return cal.fg_batch(X0) if hasattr(cal, "fg_batch") else fg_from_losses(cal, X0)
 
 
-def _fg_per_start(cal, ids, X0, gens, pending):
+def _fg_per_start(cal, ids, X0, gens, pending, exc=None):
     """A group request that raised (a subclass's loss): the reference runs each start in its own
     try/except (lbfgs_calibrator.py:258-317), so only a start whose own request raises is dropped.
-    Re-evaluate the group's starts one at a time (a start's values do not depend on the batch),
-    drop the raising ones and return the survivors' (ids, f0, G, lows)."""
+    With ``exc`` a _StartRaised (per-point compute_loss), the starts before the raising one keep
+    the losses already computed, the raising start is dropped and the evaluation goes on after it
+    -- every point evaluated exactly once.  Otherwise (a loss_batch override, which evaluates the
+    group at once) the group's starts are re-evaluated one at a time (a start's values do not
+    depend on the batch) and the raising ones dropped.  -> the survivors' (ids, f0, G, lows)."""
     keep, rows = [], []
-    for j, sid in enumerate(ids):
-        try:
-            rows.append(_fg(cal, X0[j:j + 1]))
-            keep.append(sid)
-        except _native.NativeError:
-            raise
-        except Exception:              # noqa: BLE001 -- reference: except -> continue
-            gens[sid].close()
-            del pending[sid]
+
+    def one_by_one(js):
+        for j in js:
+            try:
+                rows.append(_fg(cal, X0[j:j + 1]))
+                keep.append(ids[j])
+            except _native.NativeError:
+                raise
+            except Exception:          # noqa: BLE001 -- reference: except -> continue
+                gens[ids[j]].close()
+                del pending[ids[j]]
+
+    if not isinstance(exc, _StartRaised):
+        one_by_one(range(len(ids)))
+    off = 0
+    while isinstance(exc, _StartRaised):
+        j = off + exc.j
+        if exc.j:
+            _, dx = fd_request_points_many(X0[off:j])
+            rows.append(_fg_rows(exc.rows, dx))
+            keep.extend(ids[off:j])
+        gens[ids[j]].close()
+        del pending[ids[j]]
+        off, exc = j + 1, None
+        if off < len(ids):
+            try:
+                rows.append(_fg(cal, X0[off:]))
+                keep.extend(ids[off:])
+            except _native.NativeError:
+                raise
+            except _StartRaised as nxt:
+                exc = nxt
+            except Exception:          # noqa: BLE001 -- not the per-point path: one by one
+                one_by_one(range(off, len(ids)))
     if not keep:
         return keep, None, None, None
     return (keep, np.concatenate([r[0] for r in rows]), np.concatenate([r[1] for r in rows]),
@@ -570,8 +628,8 @@ def _advance(cal, gens, states, order, outcomes):
                 f0, G, lows = _fg(cal, X0)
             except _native.NativeError:
                 raise
-            except Exception:          # some start's loss raised: drop that start only
-                ids, f0, G, lows = _fg_per_start(cal, ids, X0, gens, pending)
+            except Exception as exc:   # some start's loss raised: drop that start only
+                ids, f0, G, lows = _fg_per_start(cal, ids, X0, gens, pending, exc)
                 if not ids:
                     continue
             launches += 1

@@ -63,3 +63,46 @@ def test_bench_line_contract_two_ranks():
     per_step = line["config"]["prices_per_step"]
     got = line["value"] * line["ms_per_step"] * 1e-3
     assert abs(got - 2 * per_step) <= 1e-6 * per_step     # prices_per_step is per rank
+
+
+@pytest.mark.gpu
+def test_bench_self_launches_ranks():
+    """`bench.py --gpus 2` without an external launcher starts its two ranks itself (child
+    processes under torch.distributed.run) and reports the world the process group saw; gloo
+    lets both ranks share the box's one GPU."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c1",
+           "--steps", "5", "--warmup", "2", "--no-calib", "--backend", "gloo"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["world_size_seen"] == 2
+
+
+def _bench_rc(args, env_extra=None, timeout=120):
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
+    if not env_extra or "WORLD_SIZE" not in env_extra:
+        env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def test_bench_world_mismatch_fails():
+    """A launcher's world that differs from --gpus is an error, not a silent one-rank run."""
+    out = _bench_rc(["--gpus", "1", "--config", "c1", "--no-cpu"],
+                    {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in out.stderr
+
+
+def test_bench_rccl_ranks_need_their_gpus():
+    """--gpus 2 under RCCL (the default backend) on a host with fewer than two GPUs fails loudly
+    in every rank instead of running on a shared device (here: no GPU at all)."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("host has two GPUs")
+    out = _bench_rc(["--gpus", "2", "--config", "c1", "--no-cpu", "--no-calib"])
+    assert out.returncode != 0
+    assert "needs 2 visible GPUs" in out.stderr

@@ -72,3 +72,48 @@ def test_subclass_compute_loss_is_what_calibrate_optimises(calib_golden):
     f, g, low = cal.fg_batch(x0[None, :])
     assert f[0] == cal.compute_loss(x0)
     assert np.all(np.isfinite(g))
+
+
+class CountingRaisingCal(RaisingCal):
+    """RaisingCal that records every point its compute_loss evaluates (raising ones too)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.seen = []
+
+    def compute_loss(self, x):
+        self.seen.append(np.array(x, copy=True))
+        return super().compute_loss(x)
+
+
+class CountingCal(OracleLossCal):
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.seen = []
+
+    def compute_loss(self, x):
+        self.seen.append(np.array(x, copy=True))
+        return super().compute_loss(x)
+
+
+def test_raising_start_costs_no_duplicate_evaluations(calib_golden):
+    """A start raising in the middle of a lockstep group: the starts before it keep the losses
+    already computed and the group goes on after it, so every point is evaluated exactly once --
+    the reference's per-start minimize calls (a re-evaluation had counted the earlier
+    starts' points twice in the subclass's side effects).  The raising start's points up to the
+    raise are evaluated once too, as the reference's would be."""
+    mkt = calib_golden["test_market"]
+    np.random.seed(0)
+    x0s = OracleLossCal(100.0, 0.05, mkt, N=N_CPU).start_points(3)
+    x0s = [x0s[0], x0s[2], x0s[1]]                  # the raising start (mu_j = -0.03) in the middle
+    cal = CountingRaisingCal(100.0, 0.05, mkt, N=N_CPU)
+    got = run_starts(cal, x0s, 2, lockstep=True)
+    ref = CountingCal(100.0, 0.05, mkt, N=N_CPU)
+    want = run_starts(ref, [x0s[0], x0s[2]], 2, lockstep=True)
+    assert got[1] is None
+    _same(got[0][0], want[0][0])
+    _same(got[2][0], want[1][0])
+    ok = [x for x in cal.seen if x[11] <= -0.0315]
+    bad = [x for x in cal.seen if x[11] > -0.0315]
+    assert len(ok) == len(ref.seen)                 # no point of a surviving start twice
+    assert len(bad) == 1                            # the raising start: its first point only

@@ -4,6 +4,7 @@ double_heston.py:48-97 restated): |phi(u)| <= M(u) = prod_i E[exp(-u^2 (1 - rho_
 (the CIR Laplace transform of each factor's integrated variance), M decreasing in u.  So a
 table's entries past the first passing candidate are below the tail cut's delta, and the
 kernels may skip evaluating them.  CPU only."""
+import mpmath as mp
 import numpy as np
 import pytest
 
@@ -50,19 +51,97 @@ def test_cf_modulus_below_laplace_bound(seed):
 
 
 def test_fp32_bound_within_margin():
-    """The kernels test the bound in fp32 against log(delta / 2) - 0.01: the fp32 log-bound must
-    stay within that margin of the fp64 one where the test is decided (log-bound > -1e3)."""
+    """The kernels test the bound in fp32 (cir_log_laplace_f32, the kernel's form) against
+    log(delta / 2) - 0.01: the fp32 log-bound must stay within that margin of the fp64 one where
+    the test is decided (log-bound > -1e3), on the generator's ranges."""
     rs = np.random.RandomState(9)
     worst = 0.0
-    for _ in range(200):
+    for _ in range(100):
         prm = LO + (HI - LO) * rs.rand(13)
         tau = rs.choice([0.02, 0.1, 0.5, 1.0, 2.0, 5.0])
-        u = np.geomspace(1.0, 3000.0, 400)
+        u = np.geomspace(1.0, 3000.0, 60)
         l64 = log_bound(prm, u, tau) + np.log(2 * 100.0 / (4.0 * (1 + u * u)))
-        with np.errstate(all="ignore"):
-            l32 = (log_bound(prm.astype(np.float32), u.astype(np.float32), np.float32(tau)) +
-                   np.log(np.float32(2 * 100.0) / (np.float32(4.0) * (1 + u.astype(np.float32) ** 2))))
+        v01, k1, t1, s1, r1, v02, k2, t2, s2, r2 = prm[:10]
+        f = np.float32
+        l32 = np.array([
+            cir_log_laplace_f32(f(0.5) * f(uu) * f(uu) * (f(1) - f(r1) * f(r1)), tau, v01, k1, t1,
+                                s1) +
+            cir_log_laplace_f32(f(0.5) * f(uu) * f(uu) * (f(1) - f(r2) * f(r2)), tau, v02, k2, t2,
+                                s2) +
+            float(np.log(f(2 * 100.0) / (f(4.0) * (f(1) + f(uu) ** 2)))) for uu in u])
         sel = l64 > -1e3
-        worst = max(worst, float(np.max(np.abs(l32[sel].astype(np.float64) - l64[sel]))))
+        worst = max(worst, float(np.max(np.abs(l32[sel] - l64[sel]))))
     print("max |fp32 - fp64| log-bound", worst)
     assert worst < 1e-3
+
+
+def cir_log_laplace_f32(s, tau, v0, kap, th, sig):
+    """csrc/dh_kernels.hip cir_log_laplace (the cancellation-free form) in fp32, operation for
+    operation (NumPy's correctly rounded exp / log stand in for the native-rate v_exp / v_log)."""
+    f = np.float32
+    s, tau, v0, kap, th, sig = (f(v) for v in (s, tau, v0, kap, th, sig))
+    with np.errstate(all="ignore"):
+        s2 = sig * sig
+        g = np.sqrt(kap * kap + f(2) * s2 * s)
+        gk = g + kap
+        x = g * tau
+        if x < 1:
+            p = f(1 / 39916800)
+            for c in (1 / 3628800, 1 / 362880, 1 / 40320, 1 / 5040, 1 / 720, 1 / 120, 1 / 24,
+                      1 / 6, 0.5):
+                p = p * -x + f(c)
+            h = p * (x * x)
+            om = x - h
+            e = f(1) - om
+        else:
+            e = np.exp(-x)
+            om = f(1) - e
+            h = x - om
+        y = (s2 * s * om) / (gk * g)
+        if y < 0.125:
+            q = f(1 / 9)
+            for c in (1 / 8, 1 / 7, 1 / 6, 1 / 5, 0.25, 1 / 3, 0.5):
+                q = q * y + f(c)
+            rm1 = q * y
+        else:
+            rm1 = (-np.log(f(1) - y) - y) / y
+        D = (h - om * rm1) / g
+        A = -((f(2) * kap * th * s) / gk) * D
+        B = (f(2) * s * om) / (gk * om + f(2) * g * e)
+        return float(A - B * v0)
+
+
+def cir_log_laplace_mp(s, tau, v0, kap, th, sig):
+    """The textbook form at 60 digits: the exact value the fp32 forms are held to."""
+    with mp.workdps(60):
+        s, tau, v0, kap, th, sig = (mp.mpf(float(v)) for v in (s, tau, v0, kap, th, sig))
+        g = mp.sqrt(kap * kap + 2 * sig * sig * s)
+        e = mp.exp(-g * tau)
+        den = (g + kap) * (1 - e) + 2 * g * e
+        A = (2 * kap * th / (sig * sig)) * (mp.log(2 * g) + (kap - g) * tau / 2 - mp.log(den))
+        return float(A - 2 * s * (1 - e) / den * v0)
+
+
+def test_fp32_bound_small_vol_of_vol():
+    """at small vol-of-vol the textbook A = (2 kappa theta / sigma^2)[...] scales the
+    fp32 rounding of a difference of O(1) logs by 2 kappa theta / sigma^2 (off by ~3 in the log at
+    sigma = 1e-4), so a candidate could pass early and the CF cut drop terms that matter.  The
+    kernel's cancellation-free form stays within 1e-4 relative of the exact log-bound for sigma
+    down to 1e-6 (kappa theta / sigma^2 up to ~1e11), kappa from 1e-4, maturities 0.01..5 and v0
+    of 0 -- far inside the 0.01 log-margin of the test."""
+    rs = np.random.RandomState(11)
+    worst, n = 0.0, 0
+    for _ in range(1500):
+        sig = 10 ** rs.uniform(-6, np.log10(0.05)) if rs.rand() < 0.7 else 10 ** rs.uniform(-1.3, 0.3)
+        kap, th = 10 ** rs.uniform(-4, 1), 10 ** rs.uniform(-3, -0.5)
+        v0 = 0.0 if rs.rand() < 0.3 else 10 ** rs.uniform(-3, -0.5)
+        tau, u, rho = 10 ** rs.uniform(-2, 0.7), 10 ** rs.uniform(0, 4), rs.uniform(-0.99, 0.99)
+        s = 0.5 * u * u * (1 - rho * rho)
+        exact = cir_log_laplace_mp(s, tau, v0, kap, th, sig)
+        if exact < -1e3:                 # far past any threshold: not where the test decides
+            continue
+        got = cir_log_laplace_f32(s, tau, v0, kap, th, sig)
+        worst = max(worst, abs(got - exact) / max(1.0, abs(exact)))
+        n += 1
+    print(f"max rel |fp32 - exact| log-bound over {n} points: {worst:.2e}")
+    assert n > 500 and worst < 1e-4

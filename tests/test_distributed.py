@@ -198,3 +198,28 @@ def test_missing_outcome_record_never_wins():
     assert d[1] == 3 and np.isnan(d[2])
     s, out, stats = D._decode(rec)
     assert s == 3 and out is None and stats == (0, np.inf)
+
+
+def test_resolve_device_under_process_group(monkeypatch):
+    """Under torch.distributed on a multi-GPU node: a gloo job that never binds a device puts
+    rank LOCAL_RANK on its own GPU (not every rank on torch's default GPU 0); a device moved with
+    torch.cuda.set_device wins over LOCAL_RANK.  (GPUs simulated: 8 visible.)"""
+    import torch
+    from dhcos import _native
+    monkeypatch.delenv("DHCOS_DEVICE", raising=False)
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    monkeypatch.setattr(_native, "device_count", lambda: 8)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    cur = {"dev": 0}
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: cur["dev"])
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        assert _native.resolve_device() == 3          # unbound: LOCAL_RANK
+        cur["dev"] = 5
+        assert _native.resolve_device() == 5          # set_device(5)
+        monkeypatch.setenv("LOCAL_RANK", "11")
+        cur["dev"] = 0
+        assert _native.resolve_device() == 3          # modulo the visible GPUs
+    finally:
+        dist.destroy_process_group()

@@ -642,6 +642,47 @@ def test_cf_cut_extreme_parameters(dh, N):
             np.max(np.abs(cut[p][good] - want[good]))
 
 
+@pytest.mark.parametrize("N", [256, 512])
+def test_cf_cut_small_vol_of_vol(dh, N):
+    """the fp32 CF-cut bound at small vol-of-vol.  The textbook CIR exponent scales a
+    difference of O(1) logs by 2 kappa theta / sigma^2, whose fp32 rounding could pass a candidate
+    early and cut CF entries that matter.  With the kernel's cancellation-free form, sets with
+    sigma down to 1e-6 (the calibrator's sigma = exp(x) reaches there in line searches) price within
+    1e-13 K of the uncut kernels, and match the oracle at the fidelity bar where the oracle's own
+    fp64 CF is accurate (sigma >= 1e-4)."""
+    from dhcos import _native
+    rs = np.random.RandomState(5 + N)
+    sig = [(1e-4, 0.3), (0.3, 1e-4), (1e-3, 2e-4), (1e-5, 1e-5), (1e-6, 0.02), (3e-4, 3e-4)]
+    P = len(sig)
+    params = np.empty((P, 13))
+    for i, (s1, s2) in enumerate(sig):
+        params[i] = [0.02 + 0.05 * rs.rand(), 0.5 + 4 * rs.rand(), 0.02 + 0.05 * rs.rand(), s1,
+                     -0.7 * rs.rand(), 0.02 + 0.05 * rs.rand(), 0.3 + rs.rand(),
+                     0.02 + 0.05 * rs.rand(), s2, -0.5 * rs.rand(), 0.1, -0.05, 0.08]
+    rec = np.zeros((P, 16))
+    rec[:, :13], rec[:, 13], rec[:, 14] = params, 100.0, 0.03
+    K = 100.0 * rs.uniform(0.85, 1.15, 200)
+    T = rs.choice([0.05, 0.25, 1.0, 3.0], 200)
+    call = rs.rand(200) < 0.5
+    ctx = _native.default_context()
+    surf = _native.Surface(ctx, K, T, call)
+    cut = surf.price(rec, N)
+    ctx.set_tail_cut(False)
+    try:
+        full = surf.price(rec, N)
+    finally:
+        ctx.set_tail_cut(True)
+    assert np.all(np.isfinite(cut)) and np.all(np.isfinite(full))
+    d = np.abs(cut - full)
+    print(f"N={N}: max |cut - full| {d.max():.3e}")
+    assert np.all(d <= 1e-13 * K[None, :]), d.max()
+    for p in range(P):
+        if min(sig[p]) < 1e-4:
+            continue
+        want = O.price_many(params[p], 100.0, K, T, 0.03, call, N)
+        assert rel_close(cut[p], want, BAR_RTOL, BAR_ATOL).all(), np.max(np.abs(cut[p] - want))
+
+
 def test_clamped_options_across_mask_words_and_tiles(dh):
     """The table kernel decides and prices clamp-widened options (double_heston.py:135-137) and
     the option kernel looks them up by a per-(p, group) bit mask.  One maturity group of 300
