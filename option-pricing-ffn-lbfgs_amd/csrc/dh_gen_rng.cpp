@@ -18,6 +18,7 @@
 // so the global stream continues exactly where the reference's loop would leave it.  No FMA
 // contraction (the Makefile builds this file with -ffp-contract=off), libm log / sqrt as NumPy.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -276,6 +277,505 @@ constexpr int64_t kSplitMin = 4096;
 
 namespace {
 
+// ---------------------------------------------------------------------------------------------
+// Parallel draw (round 4).  The stream positions of the samples are data dependent only through
+// the polar method's acceptances: a sample takes 13 doubles (its uniforms) and then candidate
+// pairs until its fresh gauss calls are served, each accepted pair serving two calls.  So:
+//   1. a twister thread runs the MT19937 recurrence alone (the only inherently serial arithmetic)
+//      and publishes the key at every 64th generation (a "block");
+//   2. bit workers re-create each block's 64 generations from its key and mark, for every double
+//      t of the stream, whether the candidate pair (D[t], D[t + 1]) is accepted (two bitmaps, by
+//      the parity of t: a sample's pairs start at t, t + 2, ... of one parity);
+//   3. the walker steps through the samples on those bits (13 doubles, then the k-th accepted
+//      candidate by popcount), recording each 64k-sample chunk's start (double index, has_gauss);
+//   4. chunk workers re-create the generator at their chunk's start and draw the chunk exactly as
+//      the sequential loop would (uniforms, accepted pairs, log / sqrt, noise), leaving the
+//      values that carry across samples -- the AR(1) blend, the spot walk and a gauss value cached
+//      across the chunk boundary -- to
+//   5. the sweep (the walker's thread, in chunk order), which also publishes the finished rows.
+// Every value comes from the same words by the same operations in the same order as in the
+// sequential draw, so the bits and the final RNG state are the same (tests/test_generator_rng.py).
+// ---------------------------------------------------------------------------------------------
+inline uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+// the MT19937 recurrence on a key (LegacyRng::twist's arithmetic), built for AVX2 and baseline
+// x86-64 (integer only: the same words either way), chosen at run time
+#define DH_TWIST_BODY                                                                             \
+    int i = 0;                                                                                    \
+    uint32_t y;                                                                                   \
+    for (; i < kMtN - kMtM; ++i) {                                                                \
+        y = (key[i] & kUpper) | (key[i + 1] & kLower);                                            \
+        key[i] = key[i + kMtM] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);                               \
+    }                                                                                             \
+    for (; i < kMtN - 1; ++i) {                                                                   \
+        y = (key[i] & kUpper) | (key[i + 1] & kLower);                                            \
+        key[i] = key[i + (kMtM - kMtN)] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);                      \
+    }                                                                                             \
+    y = (key[kMtN - 1] & kUpper) | (key[0] & kLower);                                             \
+    key[kMtN - 1] = key[kMtM - 1] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+__attribute__((target("avx2"))) void mt_twist_avx2(uint32_t* __restrict key) { DH_TWIST_BODY }
+void mt_twist_base(uint32_t* __restrict key) { DH_TWIST_BODY }
+#undef DH_TWIST_BODY
+inline void mt_twist(uint32_t* key) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) mt_twist_avx2(key);
+    else mt_twist_base(key);
+}
+
+inline double mt_double(uint32_t w0, uint32_t w1) {
+    const int32_t a = (int32_t)(w0 >> 5), b = (int32_t)(w1 >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+inline bool polar_accept(double d0, double d1) {
+    const double x1 = 2.0 * d0 - 1.0, x2 = 2.0 * d1 - 1.0;
+    const double r2 = x1 * x1 + x2 * x2;
+    return r2 < 1.0 && r2 != 0.0;
+}
+
+constexpr int kGensPerBlock = 64;
+constexpr int64_t kBlockWords = (int64_t)kGensPerBlock * kMtN;
+
+inline void spin_pause() { std::this_thread::yield(); }
+
+// how far (blocks, ~600 samples each) the twister and the bit workers may run ahead of the
+// walker: far enough that the walker never waits on them, not so far that the draw's end wastes
+// the work of many blocks past the last sample
+constexpr int64_t kLookahead = 64;
+// samples per chunk of the parallel draw (its last chunk is the draw's tail)
+constexpr int64_t kParChunk = 1 << 14;
+
+// index of the (k+1)-th set bit of w (w has more than k set bits)
+inline int select_bit(uint64_t w, int k) {
+    for (int j = 0; j < k; ++j) w &= w - 1;
+    return __builtin_ctzll(w);
+}
+
+struct ParDraw {
+    // geometry: word n >= 0 of the stream is key word (pos0 + n) % 624 of generation
+    // (pos0 + n) / 624; generation 0 is the entry key (after a pending twist)
+    int pos0 = 0;
+    uint32_t key0[kMtN];
+    int64_t n = 0, n_opt = 0, n_chunks = 0, max_t = 0, max_blocks = 0;
+    // published by the twister: keys of generations 64 b
+    std::vector<uint32_t> snaps;
+    std::atomic<int64_t> snaps_ready{0};
+    // acceptance bits of the candidate pair at double t, by parity: bit (t >> 1) of bits[t & 1]
+    std::vector<std::atomic<uint64_t>> bits[2];
+    std::vector<std::atomic<uint8_t>> block_done;
+    std::atomic<int64_t> next_block{0};
+    std::atomic<int64_t> walker_block{0};
+    // the walk's chunk starts
+    std::vector<int64_t> chunk_t;
+    std::vector<int32_t> chunk_hg;
+    std::atomic<int64_t> chunks_located{0};
+    std::atomic<int64_t> next_chunk{0};
+    std::vector<std::atomic<uint8_t>> chunk_done;
+    std::vector<double> chunk_last_gc;      // the chunk's last pair's f x1 (NaN: no pair)
+    // the chunk's gauss call served by the value cached before the chunk (at most one: after it
+    // has_gauss is 0, so the next call draws a pair): sample, and -1 (spot return) or the option
+    std::vector<int64_t> chunk_fb_i;
+    std::vector<int32_t> chunk_fb_j;
+    std::atomic<bool> walk_done{false}, failed{false};
+    int64_t t_end = 0;
+    int hg_end = 0;
+
+    // the first double of the block's range, and the block of double t
+    int64_t block_t0(int64_t b) const {
+        const int64_t w = std::max<int64_t>(0, b * kBlockWords - pos0);
+        return (w + 1) / 2;
+    }
+    int64_t block_of(int64_t t) const { return (pos0 + 2 * t) / kBlockWords; }
+
+    // key of generation g into k (from the block's snapshot, twisted forward)
+    void gen_key(int64_t g, uint32_t* k) const {
+        std::memcpy(k, snaps.data() + (g / kGensPerBlock) * kMtN, sizeof(uint32_t) * kMtN);
+        LegacyRng r;
+        std::memcpy(r.key, k, sizeof(r.key));
+        for (int64_t i = 0; i < g % kGensPerBlock; ++i) mt_twist(r.key);
+        std::memcpy(k, r.key, sizeof(r.key));
+    }
+};
+
+void par_twister(ParDraw& P) {
+    LegacyRng r;
+    std::memcpy(r.key, P.key0, sizeof(r.key));
+    for (int64_t b = 0; b < P.max_blocks; ++b) {
+        // stay a bounded distance ahead of the walker
+        while (b > P.walker_block.load(std::memory_order_acquire) + kLookahead) {
+            if (P.walk_done.load(std::memory_order_acquire) || P.failed.load()) return;
+            spin_pause();
+        }
+        if (P.walk_done.load(std::memory_order_acquire) || P.failed.load()) return;
+        if (b > 0)
+            for (int i = 0; i < kGensPerBlock; ++i) mt_twist(r.key);
+        std::memcpy(P.snaps.data() + b * kMtN, r.key, sizeof(r.key));
+        P.snaps_ready.store(b + 1, std::memory_order_release);
+    }
+}
+
+// A block's arithmetic as straight loops the compiler vectorises: the tempering, the doubles of
+// the block's range, and per parity the acceptance of each candidate pair packed 64 to a word.
+// Built twice (AVX2 and baseline x86-64, chosen at run time): integer and exactly rounded fp64
+// operations only, so both give the same bits.
+#define DH_PAR_BITS_BODY                                                                          \
+    for (int64_t j = 0; j < nw; ++j) w[j] = mt_temper(w[j]);                                     \
+    for (int64_t j = 0; j < nd; ++j) d[j] = mt_double(w[q0 + 2 * j], w[q0 + 2 * j + 1]);         \
+    for (int p = 0; p < 2; ++p) {                                                                 \
+        /* candidates t = 2 i + p in [t0, t1): doubles d[t - t0], d[t - t0 + 1] */                \
+        const int64_t i0 = (t0 - p + 1) >> 1, i1 = (t1 - p + 1) >> 1;                             \
+        for (int64_t i = i0; i < i1;) {                                                           \
+            const int64_t wend = std::min(i1, ((i >> 6) + 1) << 6);                              \
+            const int64_t cnt = wend - i;                                                         \
+            const double* dd = d + (2 * i + p - t0);                                              \
+            for (int64_t j = 0; j < cnt; ++j) {                                                   \
+                const double x1 = 2.0 * dd[2 * j] - 1.0, x2 = 2.0 * dd[2 * j + 1] - 1.0;          \
+                const double r2 = x1 * x1 + x2 * x2;                                              \
+                ok[j] = (uint8_t)((r2 < 1.0) & (r2 != 0.0));                                      \
+            }                                                                                     \
+            uint64_t m = 0;                                                                       \
+            for (int64_t j = 0; j < cnt; ++j) m |= (uint64_t)ok[j] << j;                         \
+            m <<= (i & 63);                                                                       \
+            if (m) bits[p][i >> 6].fetch_or(m, std::memory_order_relaxed);                        \
+            i = wend;                                                                             \
+        }                                                                                         \
+    }
+
+__attribute__((target("avx2"))) void par_bits_avx2(uint32_t* w, int64_t nw, double* d,
+                                                   int64_t nd, int64_t q0, int64_t t0,
+                                                   int64_t t1, uint8_t* ok,
+                                                   std::vector<std::atomic<uint64_t>>* bits) {
+    DH_PAR_BITS_BODY
+}
+
+void par_bits_base(uint32_t* w, int64_t nw, double* d, int64_t nd, int64_t q0, int64_t t0,
+                   int64_t t1, uint8_t* ok, std::vector<std::atomic<uint64_t>>* bits) {
+    DH_PAR_BITS_BODY
+}
+#undef DH_PAR_BITS_BODY
+
+struct BitsScratch {
+    std::vector<uint32_t> w;
+    std::vector<double> d;
+    uint8_t ok[64];
+};
+
+void par_bits(ParDraw& P, int64_t b, BitsScratch& S) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    // raw key words of generations 64 b .. 64 b + 64 (the next block's first words close the
+    // block's last pairs), tempered in place by the body
+    LegacyRng r;
+    std::memcpy(r.key, P.snaps.data() + b * kMtN, sizeof(r.key));
+    const int64_t nw = kBlockWords + kMtN;
+    S.w.resize(nw);
+    for (int gi = 0; gi <= kGensPerBlock; ++gi) {
+        if (gi > 0) mt_twist(r.key);
+        std::memcpy(S.w.data() + (int64_t)gi * kMtN, r.key, sizeof(r.key));
+    }
+    const int64_t base = b * kBlockWords - P.pos0;          // word n at w[n - base]
+    const int64_t t0 = P.block_t0(b), t1 = std::min(P.block_t0(b + 1), P.max_t);
+    const int64_t nd = t1 - t0 + 1;                          // doubles t0 .. t1
+    S.d.resize(nd);
+    const int64_t q0 = 2 * t0 - base;
+    if (avx2)
+        par_bits_avx2(S.w.data(), nw, S.d.data(), nd, q0, t0, t1, S.ok, P.bits);
+    else
+        par_bits_base(S.w.data(), nw, S.d.data(), nd, q0, t0, t1, S.ok, P.bits);
+    P.block_done[b].store(1, std::memory_order_release);
+}
+
+// The k-th accepted candidate pair at t, t + 2, ... (k >= 1) -> the double after it; *ok false
+// when the stream bound is reached (the caller falls back to the sequential draw)
+int64_t par_select(ParDraw& P, int64_t t, int k, int64_t& ready_t, int64_t& next_b,
+                   int64_t& last_pair, bool& ok) {
+    const int p = (int)(t & 1);
+    int64_t idx = t >> 1;
+    for (;;) {
+        const int64_t wend = ((idx >> 6) + 1) << 6;          // the word's bits are final once
+        const int64_t need_t = 2 * wend + 2;                  // its last double's pair is set
+        while (ready_t < std::min(need_t, P.max_t)) {
+            if (next_b >= P.max_blocks) break;
+            if (P.block_done[next_b].load(std::memory_order_acquire)) {
+                ++next_b;
+                ready_t = P.block_t0(next_b);
+                P.walker_block.store(next_b, std::memory_order_release);
+            } else {
+                spin_pause();
+            }
+        }
+        if (2 * wend + 1 >= P.max_t) {
+            ok = false;
+            return t;
+        }
+        const uint64_t w = P.bits[p][idx >> 6].load(std::memory_order_relaxed) >> (idx & 63);
+        const int c = __builtin_popcountll(w);
+        if (c >= k) {
+            const int64_t j = idx + select_bit(w, k - 1);
+            last_pair = 2 * j + p;
+            return last_pair + 2;
+        }
+        k -= c;
+        idx = wend;
+    }
+}
+
+void par_walk(ParDraw& P, int hg0, int64_t chunk) {
+    int64_t t = 0, ready_t = 0, next_b = 0, last_pair = -1;
+    int hg = hg0;
+    bool ok = true;
+    for (int64_t i = 0; i < P.n && ok; ++i) {
+        if (i % chunk == 0) {
+            const int64_t c = i / chunk;
+            P.chunk_t[c] = t;
+            P.chunk_hg[c] = hg;
+            P.chunks_located.store(c + 1, std::memory_order_release);
+        }
+        t += 13;                                              // :100-102
+        const int calls = (int)P.n_opt + (i > 0 ? 1 : 0);     // :112-116, :141
+        const int fresh = calls - hg;
+        if (fresh > 0) {
+            t = par_select(P, t, (fresh + 1) / 2, ready_t, next_b, last_pair, ok);
+            hg = fresh & 1;
+        } else {
+            hg -= calls;
+        }
+    }
+    if (!ok || t >= P.max_t) {
+        P.failed.store(true);
+    }
+    P.t_end = t;
+    P.hg_end = hg;
+    P.walk_done.store(true, std::memory_order_release);
+}
+
+struct ChunkOut {
+    std::vector<double> px1, px2, pr2, gn, gc;
+};
+
+// one chunk of the draw from its located start: raw uniforms into params (the blend is the
+// sweep's), noise, and the spot return's normal (ret_mu + ret_sigma g) into spots; a first gauss
+// call served from the value cached before the chunk is left to the sweep
+void par_chunk(ParDraw& P, int64_t c, int64_t chunk, const double* lo, const double* range,
+               double ret_mu, double ret_sigma, double noise_sigma, double* params,
+               double* spots, double* noise, ChunkOut& o) {
+    const int64_t c0 = c * chunk, c1 = std::min(P.n, c0 + chunk);
+    const int64_t word = P.pos0 + 2 * P.chunk_t[c];
+    LegacyRng g;
+    // the block's key may not be published yet (chunk 0 is located before the twister's first
+    // store)
+    while (P.snaps_ready.load(std::memory_order_acquire) <= (word / kMtN) / kGensPerBlock)
+        spin_pause();
+    P.gen_key(word / kMtN, g.key);
+    g.pos = (int)(word % kMtN);
+    g.has_gauss = 0;
+    g.gauss = 0.0;
+    const int64_t n_opt = P.n_opt;
+    const int64_t per = n_opt + 1;
+    const int64_t cap = (c1 - c0) * per;
+    o.px1.resize(cap);
+    o.px2.resize(cap);
+    o.pr2.resize(cap);
+    o.gn.resize(cap);
+    o.gc.resize(cap);
+    DoubleStream ds(g);
+    int hg = P.chunk_hg[c];
+    int32_t np = 0;
+    for (int64_t i = c0; i < c1; ++i) {
+        double* p = params + i * 13;
+        for (int j = 0; j < 13; ++j) p[j] = lo[j] + range[j] * ds.next();   // :100-102
+        const int calls = (int)n_opt + (i > 0 ? 1 : 0);
+        const int fresh = calls - hg;
+        const int first = np;
+        const int cached = hg;
+        const int k = fresh > 0 ? (fresh + 1) / 2 : 0;
+        ds.pairs(k, o.px1.data() + np, o.px2.data() + np, o.pr2.data() + np);
+        for (int q = first; q < first + k; ++q)
+            pair_values(o.px1[q], o.px2[q], o.pr2[q], o.gn[q], o.gc[q]);
+        np += k;
+        hg = fresh > 0 ? (fresh & 1) : hg - calls;
+        // gauss call cc of this sample: cached first (value before the sample), then new pairs
+        // each serving f x2 then f x1
+        auto value = [&](int cc, bool& from_before) {
+            from_before = false;
+            if (cached) {
+                if (cc == 0) {
+                    if (first == 0) {                        // cached across the chunk start
+                        from_before = true;
+                        return 0.0;
+                    }
+                    return o.gc[first - 1];
+                }
+                --cc;
+            }
+            return (cc & 1) ? o.gc[first + cc / 2] : o.gn[first + cc / 2];
+        };
+        bool fb;
+        const int c00 = i > 0 ? 1 : 0;
+        if (i > 0) {
+            const double v = value(0, fb);
+            spots[i] = fb ? 0.0 : ret_mu + ret_sigma * v;
+            if (fb) P.chunk_fb_i[c] = i, P.chunk_fb_j[c] = -1;
+        }
+        double* z = noise + i * n_opt;
+        for (int j = 0; j < n_opt; ++j) {
+            const double v = value(c00 + j, fb);
+            z[j] = fb ? 0.0 : 0.0 + noise_sigma * v;
+            if (fb) P.chunk_fb_i[c] = i, P.chunk_fb_j[c] = j;
+        }
+    }
+    P.chunk_last_gc[c] = np > 0 ? o.gc[np - 1] : NAN;
+    P.chunk_done[c].store(1, std::memory_order_release);
+}
+
+// -> 1 done, 0 not applicable / bound exceeded (the caller runs the sequential draw instead)
+int gen_draw_parallel(LegacyRng& g, int64_t n_samples, const double* lo, const double* hi,
+                      int n_opt, double alpha, double spot0, double ret_mu, double ret_sigma,
+                      double noise_sigma, double* params, double* spots, double* noise,
+                      const std::function<void(int64_t)>& publish) {
+    const int nth = team_size();
+    if (nth < 3) return 0;
+    ParDraw P;
+    LegacyRng e = g;
+    if (e.pos == kMtN) e.twist();
+    P.pos0 = e.pos;
+    std::memcpy(P.key0, e.key, sizeof(P.key0));
+    P.n = n_samples;
+    P.n_opt = n_opt;
+    const int64_t chunk = kParChunk;
+    P.n_chunks = (n_samples + chunk - 1) / chunk;
+    // stream bound: twice the expected doubles (acceptance pi/4) plus slack; a walk past it
+    // (never seen: ~thousands of standard deviations) falls back to the sequential draw
+    const double per_sample = 13.0 + 2.0 * ((n_opt + 2) / 2) / 0.7853981633974483;
+    P.max_t = (int64_t)(2.0 * per_sample * (double)n_samples) + (1 << 20);
+    P.max_blocks = (P.pos0 + 2 * P.max_t) / kBlockWords + 2;
+    P.snaps.resize((size_t)P.max_blocks * kMtN);
+    const int64_t nwords = (P.max_t / 2) / 64 + 2;
+    for (int p = 0; p < 2; ++p) {
+        std::vector<std::atomic<uint64_t>> v(nwords);
+        P.bits[p].swap(v);
+        for (auto& a : P.bits[p]) a.store(0, std::memory_order_relaxed);
+    }
+    {
+        std::vector<std::atomic<uint8_t>> v(P.max_blocks);
+        P.block_done.swap(v);
+        for (auto& a : P.block_done) a.store(0, std::memory_order_relaxed);
+        std::vector<std::atomic<uint8_t>> u(P.n_chunks);
+        P.chunk_done.swap(u);
+        for (auto& a : P.chunk_done) a.store(0, std::memory_order_relaxed);
+    }
+    P.chunk_t.assign(P.n_chunks, 0);
+    P.chunk_hg.assign(P.n_chunks, 0);
+    P.chunk_last_gc.assign(P.n_chunks, NAN);
+    P.chunk_fb_i.assign(P.n_chunks, -1);
+    P.chunk_fb_j.assign(P.n_chunks, -1);
+    double range[13];
+    for (int j = 0; j < 13; ++j) range[j] = hi[j] - lo[j];
+    const double beta = 1.0 - alpha;
+    double pending = g.gauss;                 // the value cached at entry (used if has_gauss)
+    double prev_spot = spot0;
+    bool fell_back = false;
+    const double t_start = now_s();
+    double t_twist = 0.0, t_walk = 0.0;
+    Team team(nth);
+    team.run([&](int w) {
+        if (w == 1) {
+            par_twister(P);
+            t_twist = now_s() - t_start;
+            w = 2;                            // then a worker like the others
+        }
+        if (w == 0) {
+            par_walk(P, g.has_gauss ? 1 : 0, chunk);
+            t_walk = now_s() - t_start;
+            if (P.failed.load()) {
+                fell_back = true;
+                return;
+            }
+            // the sweep, in chunk order
+            for (int64_t c = 0; c < P.n_chunks; ++c) {
+                while (!P.chunk_done[c].load(std::memory_order_acquire)) {
+                    if (P.failed.load()) return;
+                    spin_pause();
+                }
+                const int64_t c0 = c * chunk, c1 = std::min(n_samples, c0 + chunk);
+                const int64_t fi = P.chunk_fb_i[c];   // served from before the chunk
+                if (fi >= 0) {
+                    if (P.chunk_fb_j[c] < 0) spots[fi] = ret_mu + ret_sigma * pending;
+                    else noise[fi * n_opt + P.chunk_fb_j[c]] = 0.0 + noise_sigma * pending;
+                }
+                // the value cached after the chunk: its last pair's f x1, or (no new pair) the
+                // one from before it
+                if (!std::isnan(P.chunk_last_gc[c])) pending = P.chunk_last_gc[c];
+                for (int64_t i = c0; i < c1; ++i) {
+                    double* p = params + i * 13;
+                    if (i > 0) {
+                        const double* q = p - 13;
+                        for (int j = 0; j < 13; ++j) p[j] = alpha * q[j] + beta * p[j];   // :105-109
+                        prev_spot = prev_spot * (1.0 + spots[i]);                         // :112-116
+                    }
+                    spots[i] = prev_spot;
+                }
+                publish(c1);
+            }
+            return;
+        }
+        BitsScratch wbuf;
+        ChunkOut out;
+        for (;;) {
+            if (P.failed.load()) return;
+            const bool walking = !P.walk_done.load(std::memory_order_acquire);
+            const int64_t b = P.next_block.load(std::memory_order_relaxed);
+            if (walking && b < P.snaps_ready.load(std::memory_order_acquire) &&
+                b <= P.walker_block.load(std::memory_order_relaxed) + kLookahead) {
+                int64_t bb = b;
+                if (P.next_block.compare_exchange_weak(bb, b + 1)) par_bits(P, b, wbuf);
+                continue;
+            }
+            const int64_t c = P.next_chunk.load(std::memory_order_relaxed);
+            if (c < P.chunks_located.load(std::memory_order_acquire)) {
+                int64_t cc = c;
+                if (P.next_chunk.compare_exchange_weak(cc, c + 1))
+                    par_chunk(P, c, chunk, lo, range, ret_mu, ret_sigma, noise_sigma, params,
+                              spots, noise, out);
+                continue;
+            }
+            if (!walking && c >= P.n_chunks) return;
+            spin_pause();
+        }
+    });
+    if (std::getenv("DHCOS_GEN_TIMING"))
+        std::fprintf(stderr, "dh_gen_draw (parallel, %d threads): %lld samples: twister %.4f s, "
+                     "walk %.4f s, total %.4f s, %lld blocks\n", nth, (long long)n_samples,
+                     t_twist, t_walk, now_s() - t_start,
+                     (long long)P.snaps_ready.load());
+    if (fell_back || P.failed.load()) return 0;
+    // the state the sequential loop leaves: word n_end = 2 t_end of the stream read
+    const int64_t n_end = 2 * P.t_end;
+    if (n_end > 0) {
+        const int64_t last = P.pos0 + n_end - 1;             // the last word read
+        const int64_t gl = last / kMtN;
+        uint32_t k[kMtN];
+        if (gl == 0) std::memcpy(k, P.key0, sizeof(k));
+        else P.gen_key(gl, k);
+        std::memcpy(g.key, k, sizeof(k));
+        g.pos = (int)(last % kMtN) + 1;                      // 1 .. 624 (624: twist pending)
+    } else {
+        g = e;
+    }
+    g.has_gauss = P.hg_end;
+    g.gauss = P.hg_end ? pending : 0.0;
+    return 1;
+}
+
+}  // namespace
+
+namespace {
+
 // done (optional): the count of leading samples whose params, spot and noise are written, stored
 // with release order after each chunk (a concurrent reader may consume those rows)
 int gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* cached_gauss,
@@ -298,6 +798,16 @@ int gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* cach
     for (int j = 0; j < 13; ++j) range[j] = hi[j] - lo[j];
     const double beta = 1.0 - alpha;                      // (1 - alpha), :108
     double spot = spot0;
+    if (n_samples >= kSplitMin &&
+        gen_draw_parallel(g, n_samples, lo, hi, n_opt, alpha, spot0, ret_mu, ret_sigma,
+                          noise_sigma, params, spots, noise, publish)) {
+        std::memcpy(mt_key, g.key, sizeof(g.key));
+        *mt_pos = g.pos;
+        *has_gauss = g.has_gauss;
+        *cached_gauss = g.gauss;
+        publish(n_samples);
+        return DH_OK;
+    }
     if (n_samples < kSplitMin) {
         for (int64_t i = 0; i < n_samples; ++i) {
             double* p = params + i * 13;

@@ -12,10 +12,11 @@ is exchanged: the shards are independent and each rank drives its own GPU.
     RNG state after the draws, so the result, ``n_calls`` / ``best_loss`` (those of the last
     start) and every rank's ``np.random`` stream afterwards equal the single-process
     ``calibrate`` with the same RNG state.
-  * ``generate_sharded``: rank 0 draws every sample's random numbers in reference order
-    (synthetic_generator.py:98-141) and broadcasts them; rank r prices a contiguous block of
-    samples; one all-gather assembles the prices on every rank; rank 0 builds and saves the
-    reference output.  Every rank's ``np.random`` ends where rank 0's draws left it.
+  * ``generate_sharded``: rank 0's ``np.random`` state is broadcast and every rank draws every
+    sample's random numbers in reference order (synthetic_generator.py:98-141) with the parallel
+    native draw; rank r prices a contiguous block of samples; one all-gather assembles the prices
+    on every rank; rank 0 builds and saves the reference output.  Every rank's ``np.random`` ends
+    where rank 0's draws left it.
 
 Only collectives on small host-side records and (generator) the price block are used; the COS
 kernels never wait on another rank.  The collectives run over ``torch.distributed`` (a process
@@ -234,17 +235,14 @@ def generate_sharded(n_samples: int = 500,
                                                  as_arrays=as_arrays, verbose=verbose)
     price_fn = price_fn or (lambda p, s: G.price_grid(p, s, N=N, device=device))
     n_opt = len(G.STRIKES_PCT) * len(G.MATURITIES)
-    width = 13 + 1 + n_opt
-    draws = None
-    if rank == 0:           # the draws, then the RNG state they leave (every rank continues there)
-        params, spots, noise = G.draw_paths(n_samples)
-        draws = np.concatenate([np.concatenate([params, spots[:, None], noise], axis=1).ravel(),
-                                _rng_state_vec()])
+    # every rank draws the whole stream itself from rank 0's RNG state (627 words broadcast; the
+    # native draw is parallel on each rank's host threads), so no rank waits for rank 0's draw
+    # and nothing of the draws crosses the links; every rank's np.random ends where rank 0's
+    # draw leaves it
     if world > 1 or comm is not None:
-        draws = _broadcast_f64(draws, (n_samples * width + 627,), group, device, comm)
-        _set_rng_state_vec(draws[n_samples * width:])
-    draws = draws[:n_samples * width].reshape(n_samples, width)
-    params, spots, noise = draws[:, :13], draws[:, 13], draws[:, 14:]
+        state = _rng_state_vec() if rank == 0 else None
+        _set_rng_state_vec(_broadcast_f64(state, (627,), group, device, comm))
+    params, spots, noise = G.draw_paths(n_samples)
     lo, hi = sample_block(n_samples, rank, world)
     block = price_fn(params[lo:hi], spots[lo:hi]) if hi > lo else np.empty((0, n_opt))
     if world > 1 or comm is not None:

@@ -186,3 +186,30 @@ def test_native_assemble_equals_numpy(n, m):
     assert np.array_equal(loss, np.array([np.mean(((model[i] - want_mkt[i]) / want_mkt[i]) ** 2)
                                           for i in range(n)]))
     assert np.array_equal(strikes, (k_rel[None, :] * spots[:, None]) / 100.0)
+
+
+@pytest.mark.parametrize("n_opt,threads,pre", [(15, 3, 0), (15, 7, 1), (0, 4, 1), (1, 5, 0),
+                                               (2, 16, 1), (15, 16, 2)])
+def test_parallel_draw_equals_numpy_loop(monkeypatch, n_opt, threads, pre):
+    """The parallel draw (twister, acceptance bits, walk, chunk workers, sweep; dh_gen_rng.cpp)
+    for every team size and grid width, with and without a gauss cached at entry: the same draws
+    and the same continuation of np.random as NumPy's own per-sample loop.  n spans several of the
+    draw's 16k-sample chunks, and n_opt = 0 / 1 exercise a cached value served past a chunk's
+    first sample."""
+    monkeypatch.setenv("DHCOS_GEN_THREADS", str(threads))
+    n = 40000
+    strikes = np.arange(max(n_opt, 1))[:n_opt] + 90.0
+    mats = np.array([1.0])
+    np.random.seed(31 + n_opt)
+    for _ in range(pre):
+        np.random.normal()
+    want = G.draw_paths_numpy(n, strikes, mats)
+    after_want = np.random.random(5)
+    np.random.seed(31 + n_opt)
+    for _ in range(pre):
+        np.random.normal()
+    got = G.draw_paths(n, strikes, mats)
+    after_got = np.random.random(5)
+    for a, b in zip(got, want):
+        assert a.shape == b.shape and np.array_equal(a, b)
+    assert np.array_equal(after_got, after_want)

@@ -14,7 +14,7 @@ cd /tmp && export TMPDIR=/tmp && cd - > /dev/null || exit 1
 for c in $CONFIGS; do
   if [ $c = c5 ]; then STEPS="--steps 3 --warmup 1"; PSTEPS="--steps 1 --warmup 1"; else STEPS="--steps 100 --warmup 10"; PSTEPS="--steps 20 --warmup 3"; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o ${TAG}_${c}_stats --output-format csv \
-      -- python bench.py --config $c $STEPS --no-cpu --no-calib \
+      -- python bench.py --config $c $STEPS --no-cpu --no-calib --no-side \
       > $OUT/${TAG}_${c}_stats.log 2>&1 || { echo "stats $c failed rc=$?"; exit 1; }
   echo "stats $c ok"
   i=0
@@ -22,7 +22,7 @@ for c in $CONFIGS; do
     [ -z "$grp" ] && continue
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $OUT -o ${TAG}_${c}_pmc$i --output-format csv \
-        -- python bench.py --config $c $PSTEPS --no-cpu --no-calib \
+        -- python bench.py --config $c $PSTEPS --no-cpu --no-calib --no-side \
         > $OUT/${TAG}_${c}_pmc$i.log 2>&1 || { echo "pmc $c pass $i failed rc=$?"; exit 1; }
     echo "pmc $c pass $i ($grp) ok"
   done <<EOG
