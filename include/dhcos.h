@@ -238,6 +238,11 @@ int dh_gen_draw_progress(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,
                          const double* hi, int n_opt, double alpha, double spot0, double ret_mu,
                          double ret_sigma, double noise_sigma, double* params, double* spots,
                          double* noise, int64_t* done);
+/* The generator's trading dates (synthetic_generator.py:59-67: weekdays from a Monday, here
+ * 2022-01-03 = day 18995 since 1970-01-01, as 'YYYY-MM-DD'): sample i's date as 10 UCS-4 code
+ * points at out[10 i] (a NumPy '<U10' array's buffer).  DH_E_ARG past year 9999.             */
+int dh_gen_dates(int64_t first_day, int64_t n, uint32_t* out);
+
 /* The generator's host arithmetic after pricing (synthetic_generator.py:141-157), per sample i
  * and option j of [n_samples][n_opt] row-major arrays: market = model + noise * model, loss[i] =
  * mean_j ((model - market) / market)^2 formed as np.mean forms it (bit for bit), strikes =

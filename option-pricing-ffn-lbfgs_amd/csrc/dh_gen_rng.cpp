@@ -1053,3 +1053,58 @@ extern "C" int dh_gen_assemble(const double* model, const double* noise, const d
     team.run([&](int w) { sweep(n_samples * w / nt, n_samples * (w + 1) / nt); });
     return DH_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// dh_gen_dates: the generator's trading dates (synthetic_generator.py:59-67: weekdays from
+// 2022-01-03, a Monday, 'YYYY-MM-DD') as UCS-4 code points of a NumPy '<U10' array, one pass on
+// a worker team: sample i falls on day first_day + 7 (i / 5) + i % 5 (days since 1970-01-01), and
+// the civil date is H. Hinnant's days-to-civil algorithm.  Years past 9999 are the caller's
+// (NumPy formats those; the call returns DH_E_ARG).
+// ---------------------------------------------------------------------------------------------
+extern "C" int dh_gen_dates(int64_t first_day, int64_t n, uint32_t* out) {
+    if (n < 0 || (n > 0 && !out)) return DH_E_ARG;
+    if (n == 0) return DH_OK;
+    auto civil = [](int64_t z, int64_t& y, int& m, int& d) {
+        z += 719468;
+        const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+        const int64_t doe = z - era * 146097;
+        const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+        const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+        const int64_t mp = (5 * doy + 2) / 153;
+        d = (int)(doy - (153 * mp + 2) / 5 + 1);
+        m = (int)(mp < 10 ? mp + 3 : mp - 9);
+        y = yoe + era * 400 + (m <= 2);
+    };
+    {
+        int64_t y;
+        int m, d;
+        civil(first_day + 7 * ((n - 1) / 5) + (n - 1) % 5, y, m, d);
+        if (y > 9999 || first_day < 0) return DH_E_ARG;
+    }
+    auto sweep = [&](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            int64_t y;
+            int m, d;
+            civil(first_day + 7 * (i / 5) + i % 5, y, m, d);
+            uint32_t* c = out + i * 10;
+            c[0] = '0' + (uint32_t)(y / 1000);
+            c[1] = '0' + (uint32_t)(y / 100 % 10);
+            c[2] = '0' + (uint32_t)(y / 10 % 10);
+            c[3] = '0' + (uint32_t)(y % 10);
+            c[4] = '-';
+            c[5] = '0' + (uint32_t)(m / 10);
+            c[6] = '0' + (uint32_t)(m % 10);
+            c[7] = '-';
+            c[8] = '0' + (uint32_t)(d / 10);
+            c[9] = '0' + (uint32_t)(d % 10);
+        }
+    };
+    if (n < kSplitMin) {
+        sweep(0, n);
+        return DH_OK;
+    }
+    Team team(team_size());
+    const int nt = team.size();
+    team.run([&](int w) { sweep(n * w / nt, n * (w + 1) / nt); });
+    return DH_OK;
+}

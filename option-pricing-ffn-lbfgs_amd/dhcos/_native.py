@@ -87,6 +87,7 @@ SIGNATURES = {
                                        C.c_double, C.c_double, _dp, _dp, _dp,
                                        C.POINTER(C.c_int64)]),
     "dh_gen_assemble": (C.c_int, [_dp, _dp, _dp, _dp, C.c_int64, C.c_int, _dp, _dp, _dp]),
+    "dh_gen_dates": (C.c_int, [C.c_int64, C.c_int64, _vp]),
     "dh_price_batch": (C.c_int, [_vp, _dp, C.c_int64, _dp, _dp, _i8p, C.c_int, C.c_int,
                                  C.c_double, _dp]),
     "dh_loss_batch": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp, _i8p, _dp, C.c_int, C.c_double,
@@ -659,6 +660,16 @@ def gen_assemble(model, noise, spots, k_rel, out=None):
     return market, loss, strikes
 
 
+def gen_dates(first_day, n):
+    """dh_gen_dates: n weekday dates from day first_day (a Monday; days since 1970-01-01) as a
+    '<U10' array of 'YYYY-MM-DD', or None past year 9999 (the caller formats those)."""
+    out = np.empty(int(n), dtype="U10")
+    rc = load().dh_gen_dates(int(first_day), int(n), out.ctypes.data if n else None)
+    if rc != 0:
+        return None
+    return out
+
+
 _tls = threading.local()
 
 
@@ -706,7 +717,7 @@ def default_context(device: int | None = None) -> Context:
     return ctx
 
 
-__all__ = ["gen_draw", "gen_assemble", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
+__all__ = ["gen_draw", "gen_assemble", "gen_dates", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "MAX_N_PER_TERM",
            "STRIKE_ABSOLUTE",
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN", "LIB_PATH",

@@ -22,6 +22,7 @@ What changes relative to the reference, and what does not:
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from operator import itemgetter
@@ -514,16 +515,30 @@ class _StartState:
         self.best_loss = np.inf
 
 
-def _pipeline_surface(cal, n_starts):
+# prices per param set (options x COS terms) below which a request's device time is shorter than
+# the host work a second request group adds per iteration (fd_models, the ctypes calls, the
+# bookkeeping: ~20 us), so one lockstep group is faster than the two-group pipeline (C1: 15 x 128)
+PIPELINE_MIN_PRICES = 16384
+
+
+def _pipeline_surface(cal, n_starts, force=None):
     """The surface the two-group pipelined loop may use, or None: subclassed losses, markets
     without a surface, one start, or groups too large for one asynchronous request keep the
-    lockstep loop."""
+    lockstep loop; so do (force None: automatic, $DHCOS_SCIPY_PIPELINE = 0 / 1 overrides) markets
+    whose requests are too short to hide a group's host work (PIPELINE_MIN_PRICES)."""
+    if force is None:
+        env = os.environ.get("DHCOS_SCIPY_PIPELINE", "")
+        force = {"0": False, "1": True}.get(env)
+    if force is False:
+        return None
     if n_starts < 2 or -(-n_starts // 2) * (N_PARAMS + 1) > _native_async_max_sets():
         return None
     cls = type(cal)
     if (not isinstance(cal, DoubleHestonJumpCalibrator)
             or cls.fg_batch is not DoubleHestonJumpCalibrator.fg_batch
             or _custom_loss(cal) or not len(cal.market_options)):
+        return None
+    if force is None and len(cal.market_options) * getattr(cal, "N", 128) < PIPELINE_MIN_PRICES:
         return None
     return cal._get_surface()
 
@@ -533,13 +548,14 @@ def _native_async_max_sets():
 
 
 def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: bool = True,
-               pipeline: bool = True):
+               pipeline=None):
     """Run one L-BFGS-B per x0; returns [(OptimizeResult, t_done) | None] in start order.
 
     lockstep: every live start's function+gradient request shares one launch (S = 14 x live
     starts); otherwise the starts run one after the other.  pipeline (with lockstep, >= 2
-    starts): the starts form two groups whose requests alternate on the device, so one group's
-    setulb steps run on the host while the other's request runs (_advance_pipelined).  A start's
+    starts; None: by the market's size, _pipeline_surface): the starts form two groups whose
+    requests alternate on the device, so one group's setulb steps run on the host while the
+    other's request runs (_advance_pipelined).  A start's
     values depend only on its own x (the kernels are batch-composition invariant), so all three
     give the same results."""
     n = len(x0s)
@@ -549,7 +565,7 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
     gens = [lbfgsb_steps(x0, maxiter, _MAXFUN) for x0 in x0s]
     states = [_StartState() for _ in range(n)]
     order = [list(range(n))] if lockstep else [[s] for s in range(n)]
-    surf = _pipeline_surface(cal, n) if (lockstep and pipeline) else None
+    surf = _pipeline_surface(cal, n, pipeline) if (lockstep and pipeline is not False) else None
     with _single_threaded_blas():
         if surf is not None:
             _advance_pipelined(cal, surf, gens, states, outcomes)

@@ -13,6 +13,14 @@ pricer (within ~1e-13 of the reference: itself last-bit noise) and multiply ever
 (1 + eps U(-1, 1)), eps = 1e-15, each with its own seed.
 
 Usage:  python tests/golden/make_calib_noise.py [--members 12]
+        python tests/golden/make_calib_noise.py --surface 5x5 [--members 12] [--procs 6]
+The second form (round 4, VERDICT r3 "pin calibrate() on one more surface") builds a 5 x 5
+synthetic surface the way bench.py does (K/S in linspace(0.8, 1.2), T in linspace(0.1, 2.0),
+calls, S0 = 100, r = 0.03, market = the model at a seed-1 draw of the generator's ranges x
+(1 + N(0, 0.02)) with seed 2, here priced by the oracle at N = 128), takes its np.random.seed(0)
+starts from the calibrator's get_initial_guess (a NumPy restatement of lbfgs_calibrator.py:179-234
+checked against the reference's draws in tests/golden/calib.json) and writes
+tests/golden/calib_noise_5x5.json with the market and starts embedded.
 """
 import argparse
 import json
@@ -27,15 +35,16 @@ sys.path.insert(0, ROOT)
 from oracle import dh_oracle as O  # noqa: E402
 
 
-def run_start(market, x0, eps, seed, scalar=False):
+def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05):
     mk = np.array([o["price"] for o in market])
     K = [o["strike"] for o in market]
     T = [o["maturity"] for o in market]
+    call = np.array([O.is_call_type(o["option_type"]) for o in market])
     rs = np.random.RandomState(seed)
 
     def loss(x):
         p = O.to_params(x)
-        pr = O.price_many(p, 100.0, K, T, 0.05, True, 128, scalar=scalar)
+        pr = O.price_many(p, S0, K, T, r, call, 128, scalar=scalar)
         if eps:
             pr = pr * (1 + eps * rs.uniform(-1, 1, pr.size))
         if not np.all(np.isfinite(pr)) or np.any(pr <= 0):
@@ -48,16 +57,73 @@ def run_start(market, x0, eps, seed, scalar=False):
         return f[0], O.fd_grad(f, dx)
 
     with np.errstate(all="ignore"):
-        r = minimize(fg, x0, method="L-BFGS-B", jac=True,
-                     options={"maxiter": 300, "ftol": 1e-9, "gtol": 1e-6, "maxfun": 15000 // 14})
-    return {"fun": float(r.fun), "nit": int(r.nit), "nfev_requests": int(r.nfev),
-            "message": str(r.message), "success": bool(r.success)}
+        res = minimize(fg, x0, method="L-BFGS-B", jac=True,
+                       options={"maxiter": 300, "ftol": 1e-9, "gtol": 1e-6, "maxfun": 15000 // 14})
+    return {"fun": float(res.fun), "nit": int(res.nit), "nfev_requests": int(res.nfev),
+            "message": str(res.message), "success": bool(res.success)}
+
+
+GEN_LO = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
+GEN_HI = np.array([0.08, 4.5, 0.065, 0.5, -0.4, 0.07, 1.2, 0.07, 0.35, -0.2, 0.25, -0.01, 0.12])
+
+
+def surface_5x5():
+    """bench.py make_surface(5, 5) priced by the oracle (N = 128): (market, S0, r)."""
+    S0, r = 100.0, 0.03
+    kk, tt = np.meshgrid(np.linspace(0.8, 1.2, 5) * S0, np.linspace(0.1, 2.0, 5))
+    K, T = kk.ravel(), tt.ravel()
+    true = GEN_LO + (GEN_HI - GEN_LO) * np.random.RandomState(1).rand(13)
+    model = O.price_many(true, S0, K, T, r, True, 128)
+    mkt = model * (1 + np.random.RandomState(2).normal(0, 0.02, K.size))
+    return [{"strike": float(k), "maturity": float(t), "price": float(p), "option_type": "call"}
+            for k, t, p in zip(K, T, mkt)], S0, r
+
+
+def _member(args):
+    market, x0s, m, S0, r = args
+    eps = 0.0 if m == 0 else 1e-15
+    starts = [run_start(market, np.array(x0), eps, 1000 * m + s, scalar=(m == 0), S0=S0, r=r)
+              for s, x0 in enumerate(x0s)]
+    best, best_loss = None, np.inf
+    for s, st in enumerate(starts):          # lbfgs_calibrator.py:271: strict <, start order
+        if st["fun"] < best_loss:
+            best, best_loss = s, st["fun"]
+    return {"eps": eps, "pricer": "scalar" if m == 0 else "vectorised", "starts": starts,
+            "best_start": best, "final_loss": best_loss, "message": starts[best]["message"],
+            "iterations": starts[best]["nit"]}
+
+
+def main_surface(members_n, procs):
+    import multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "option-pricing-ffn-lbfgs_amd"))
+    from dhcos.calibrator import DoubleHestonJumpCalibrator   # get_initial_guess: NumPy only
+    market, S0, r = surface_5x5()
+    np.random.seed(0)
+    x0s = [x.tolist() for x in DoubleHestonJumpCalibrator(S0, r, market).start_points(3)]
+    with mp.get_context("fork").Pool(procs) as pool:
+        members = pool.map(_member, [(market, x0s, m, S0, r) for m in range(members_n)])
+    for m, mb in enumerate(members):
+        print(m, mb["best_start"], mb["final_loss"], mb["iterations"], mb["message"],
+              [(s["nit"], s["message"][:12], round(s["fun"], 12)) for s in mb["starts"]])
+    winners = [m["final_loss"] for m in members]
+    out = {"what": "calibrate(300, 3) of the reference algorithm (oracle losses at N = 128, SciPy "
+                   "L-BFGS-B) on a 5 x 5 synthetic surface (make_calib_noise.py surface_5x5), "
+                   "np.random.seed(0) starts, prices x (1 + 1e-15 U(-1, 1)) per member (member "
+                   "0: the reference-exact scalar pricer, noise-free)",
+           "market": market, "S0": S0, "r": r, "x0s": x0s,
+           "members": members, "final_loss_min": min(winners), "final_loss_max": max(winners)}
+    with open(os.path.join(ROOT, "tests", "golden", "calib_noise_5x5.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--members", type=int, default=12)
+    ap.add_argument("--surface", default=None, choices=[None, "5x5"])
+    ap.add_argument("--procs", type=int, default=6)
     a = ap.parse_args()
+    if a.surface == "5x5":
+        return main_surface(a.members, a.procs)
     with open(os.path.join(ROOT, "tests", "golden", "calib.json")) as fh:
         g = json.load(fh)
     market = g["test_market"]

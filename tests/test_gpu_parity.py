@@ -375,7 +375,7 @@ def test_lockstep_equals_sequential(dh, calib_golden):
     x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
     a = run_starts(cal, x0s, 300, lockstep=True, pipeline=False)
     launches = cal.lockstep_launches
-    p = run_starts(cal, x0s, 300, lockstep=True)
+    p = run_starts(cal, x0s, 300, lockstep=True, pipeline=True)
     p_launches = cal.lockstep_launches
     b = run_starts(cal, x0s, 300, lockstep=False)
     for (ra, _), (rp, _), (rb, _) in zip(a, p, b):
