@@ -1147,7 +1147,10 @@ template <int RT>
 __device__ __forceinline__ int group_lanes(int nopt, int N, int tpt) {
     const int R = min(RT, max(nopt, 1));
     const int ngroups = (nopt + R - 1) / R;
-    if (tpt == kBlock && RT == kR) return max(1, min(tpt / ngroups, N - 1));
+#ifndef DH_GMAX
+#define DH_GMAX 1024
+#endif
+    if (tpt == kBlock && RT == kR) return max(1, min(min(tpt / ngroups, DH_GMAX), N - 1));
     int G = 1;
     while (G * 2 <= tpt / max(ngroups, 1) && G < 64) G *= 2;
     while (G > 1 && G / 2 >= N - 1) G /= 2;                 // no more lanes than terms k >= 1

@@ -6,6 +6,8 @@ Tolerances (floating point, fp64):
   * fidelity target actually asserted on well-conditioned prices: 1e-10 relative
   * losses: 1e-9 relative; FD gradients: conftest.fd_grad_tol with price noise 1e-13
 """
+import os
+
 import numpy as np
 import pytest
 from scipy.optimize import minimize
@@ -348,6 +350,47 @@ def test_calibrate_seed0(dh, calib_golden, calib_noise):
     assert_in_noise_ensemble(r, runs, calib_noise, g["calibrate_seed0_starts"], "scipy")
     assert rel_close(r.model_prices, cal.market_prices, 5e-3, 0).all()
     assert r.calibration_time is not None and r.calibration_time < g["calibrate_seed0"]["seconds"]
+
+
+@pytest.mark.parametrize("driver", ["scipy", "device"])
+def test_calibrate_5x5_surface_in_noise_ensemble(dh, driver):
+    """calibrate(300, 3) under np.random.seed(0) on a second market: the 5 x 5 synthetic surface
+    of tests/golden/calib_noise_5x5.json (bench.py's construction at N = 128), against the
+    reference algorithm's outcomes under last-bit price noise (12 members; member 0 the
+    reference-exact scalar pricer).  Per start: the x0 the reference draws, the ensemble's
+    message and a loss inside the members' range for that start (x/ 2: 12 members sample a
+    chaotic map); start 0 (the literature guess on the Feller kink) exactly as every member;
+    the winner inside the members' band of final losses.  Per-start outcomes are printed beside
+    member 0's."""
+    import json
+    from conftest import GOLDEN
+    from dhcos.calibrator import run_starts, run_starts_device
+    with open(os.path.join(GOLDEN, "calib_noise_5x5.json")) as fh:
+        ens = json.load(fh)
+    mkt, S0, r = ens["market"], ens["S0"], ens["r"]
+    np.random.seed(0)
+    cal = dh.DoubleHestonJumpCalibrator(S0, r, mkt)
+    assert np.array_equal(np.array(cal.start_points(3)), np.array(ens["x0s"]))
+    np.random.seed(0)
+    res = dh.DoubleHestonJumpCalibrator(S0, r, mkt).calibrate(maxiter=300, multi_start=3,
+                                                                driver=driver)
+    x0s = [np.array(x) for x in ens["x0s"]]
+    c2 = dh.DoubleHestonJumpCalibrator(S0, r, mkt)
+    runs = run_starts(c2, x0s, 300) if driver == "scipy" else run_starts_device(c2, x0s, 300)
+    ref = ens["members"][0]["starts"]
+    for s, ((rr, _), want) in enumerate(zip(runs, ref)):
+        members = [m["starts"][s] for m in ens["members"]]
+        print(f"{driver} start {s}: nit {rr.nit:3d} {rr.message!r:58} fun {rr.fun:.6e}   "
+              f"member 0: nit {want['nit']:3d} {want['message']!r:58} fun {want['fun']:.6e}")
+        assert rr.message in {m["message"] for m in members}, (s, rr.message)
+        if s == 0:
+            assert rr.nit == 0 and rr.message == "ABNORMAL: "
+            assert rel_close(rr.fun, want["fun"], LOSS_RTOL, 0)
+        lo = min(m["fun"] for m in members) / 2
+        hi = max(m["fun"] for m in members) * 2
+        assert lo <= rr.fun <= hi, (s, rr.fun, lo, hi)
+    assert ens["final_loss_min"] / 2 <= res.final_loss <= ens["final_loss_max"] * 2
+    assert res.final_loss == min(rr.fun for rr, _ in runs)
 
 
 def test_robust_start_matches_reference_exactly(dh, calib_golden):
