@@ -27,6 +27,7 @@ MAX_N_PER_TERM = 65536         # longest accepted; longer than MAX_N runs the pe
 STRIKE_ABSOLUTE = 0
 STRIKE_PCT_SPOT = 1
 PATH_AUTO, PATH_SPLIT, PATH_FUSED, PATH_GEN = 0, 1, 2, 3   # PATH_GEN: reported only (AUTO)
+PATH_FUSED_MT = 4              # several tables per block (dh_ctx_set_path; AUTO on large grids)
 STAMPS_PER_BLOCK = 32          # kStamps of the DH_STAMPS build (csrc/dh_kernels.hip)
 
 _dp = C.POINTER(C.c_double)
@@ -203,8 +204,9 @@ class Context:
         _check(load().dh_ctx_set_tail_cut(self._h, 1 if on else 0))
 
     def set_path(self, path: int):
-        """Request kernels: PATH_AUTO (default), PATH_SPLIT (table + option launches) or
-        PATH_FUSED (one launch per request where every maturity group is one tile)."""
+        """Request kernels: PATH_AUTO (default), PATH_SPLIT (table + option launches),
+        PATH_FUSED (one launch per request where every maturity group is one tile) or
+        PATH_FUSED_MT (that launch with several tables per block, where it applies)."""
         _check(load().dh_ctx_set_path(self._h, int(path)))
 
     @property
@@ -720,6 +722,7 @@ def default_context(device: int | None = None) -> Context:
 __all__ = ["gen_draw", "gen_assemble", "gen_dates", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "MAX_N_PER_TERM",
            "STRIKE_ABSOLUTE",
-           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN", "LIB_PATH",
+           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN", "PATH_FUSED_MT",
+           "LIB_PATH",
            "SIGNATURES",
            "Comm", "comm_id", "best_start", "COMM_ID_BYTES"]

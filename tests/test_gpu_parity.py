@@ -831,6 +831,10 @@ def _with_path(ctx, path, fn):
                                  # fused path its 5-wave build (grids of >= 4,096 blocks)
     (49, 288, 1024, 32, 256),    # 9,216 tables: the fused blocks load their prologue constants
                                  # from table_prologue_kernel (grids of >= 8,192 blocks)
+    (50, 7, 2000, 20, 512),      # C3-like, odd param-set count: the multi-table kernel's last
+                                 # block of each group holds one table
+    (51, 43, 10000, 100, 512),   # C3 shape at 43 sets: 4,300 tables (AUTO takes the multi-table
+                                 # kernel), clamp-widened strikes in the first group
 ])
 def test_fused_equals_split_bitwise(dh, seed, P, M, n_T, N):
     """The fused single-launch request kernel and the table + option launches compute every
@@ -846,16 +850,18 @@ def test_fused_equals_split_bitwise(dh, seed, P, M, n_T, N):
     mkt = np.abs(O.price_many(params[0], 100.0, K, T, 0.03, call, N)) + 1e-3
     surf = _native.Surface(ctx, K, T, call, mkt)
     res = {}
-    for path in (_native.PATH_SPLIT, _native.PATH_FUSED):
+    for path in (_native.PATH_SPLIT, _native.PATH_FUSED, _native.PATH_FUSED_MT):
         pr = _with_path(ctx, path, lambda: surf.price(rec, N))
         sse, bad, lp = _with_path(ctx, path, lambda: surf.loss_terms(rec, N, want_prices=True))
         res[path] = (pr, sse, bad, lp)
-    s, f = res[_native.PATH_SPLIT], res[_native.PATH_FUSED]
+    s, f, mt = res[_native.PATH_SPLIT], res[_native.PATH_FUSED], res[_native.PATH_FUSED_MT]
     assert np.array_equal(surf.price(rec, N), f[0])
-    # auto: fused wherever every group is one tile (these are no generator-sized small-tile calls)
-    assert ctx.last_path == _native.PATH_FUSED
-    for a, b in zip(s, f):
+    # auto: fused wherever every group is one tile (these are no generator-sized small-tile calls),
+    # several tables per block from 2,048 tables where the multi-table kernel applies
+    assert ctx.last_path in (_native.PATH_FUSED, _native.PATH_FUSED_MT)
+    for a, b, c in zip(s, f, mt):
         assert np.array_equal(a, b), np.max(np.abs(np.asarray(a, float) - np.asarray(b, float)))
+        assert np.array_equal(a, c), np.max(np.abs(np.asarray(a, float) - np.asarray(c, float)))
     assert np.array_equal(f[0], f[3])
     for p in range(0, P, max(1, P // 3)):
         want = O.price_many(params[p], 100.0, K, T, 0.03, call, N)
