@@ -490,6 +490,66 @@ class Surface:
                                           _vp(stream) if stream else None))
 
 
+class FgChannel:
+    """One slot of dh_surface_fg_begin / _end with its arguments prepared once: preallocated
+    input (x0, model) and output (f, g, low) buffers whose addresses and the constant scalars are
+    ctypes objects built up front, so a request costs two row copies in, one foreign call each
+    way and three small copies out (the SciPy driver's per-request host path: the generic
+    Surface.fg_begin / fg_end marshal every argument per call, ~10 us each).  The slot protocol
+    (Context._fg_s, the context lock) is Surface.fg_begin / fg_end's."""
+
+    def __init__(self, surf: "Surface", slot: int, s_max: int, S0, r, N=128, L=10.0):
+        lib = load()
+        self.surf, self.slot, self.s_max = surf, int(slot), int(s_max)
+        if self.slot not in (0, 1) or self.s_max < 1:
+            raise ValueError("slot must be 0 or 1 and s_max >= 1")
+        self._x = np.empty((self.s_max, 13))
+        self._m = np.empty(2 * self.s_max * 13)        # [2][S][13] for the request's S
+        self._f, self._low = np.empty(self.s_max), np.empty(self.s_max)
+        self._g = np.empty((self.s_max, 13))
+        self._begin = lib["dh_surface_fg_begin"]        # own function objects: raw arguments
+        self._begin.restype, self._begin.argtypes = C.c_int, None
+        self._end = lib["dh_surface_fg_end"]
+        self._end.restype, self._end.argtypes = C.c_int, None
+        ctx = C.c_void_p(surf.ctx.handle.value)
+        sh = C.c_void_p(surf.handle.value)
+        self._S = C.c_int(0)
+        self._bargs = (ctx, sh, C.c_void_p(self._x.ctypes.data), C.c_void_p(self._m.ctypes.data),
+                       self._S, C.c_double(float(S0)), C.c_double(float(r)), C.c_int(int(N)),
+                       C.c_double(float(L)), C.c_int(self.slot))
+        self._eargs = (ctx, sh, C.c_int(self.slot), self._S, C.c_void_p(self._f.ctypes.data),
+                       C.c_void_p(self._g.ctypes.data), C.c_void_p(self._low.ctypes.data))
+        self._lock = surf.ctx._lock
+        self._fg_s = surf.ctx._fg_s
+
+    def model_out(self, S: int) -> np.ndarray:
+        """The [2, S, 13] model buffer of a request of S starts (fd_models(..., out=))."""
+        return self._m[:2 * S * 13].reshape(2, S, 13)
+
+    def begin(self, X0: np.ndarray, model: np.ndarray = None):
+        """Enqueue the request of X0 [S, 13] (model: [2, S, 13], default: already written into
+        model_out(S))."""
+        S = X0.shape[0]
+        if S > self.s_max or S < 1:
+            raise ValueError(f"request of {S} starts on a channel of {self.s_max}")
+        self._x[:S] = X0
+        if model is not None:
+            self.model_out(S)[...] = model
+        with self._lock:
+            self._S.value = S
+            _check(self._begin(*self._bargs))
+            self._fg_s[self.slot] = S
+
+    def end(self):
+        """-> (f [S], g [S, 13], low [S]) of the slot's request (copies: the buffers are reused)."""
+        with self._lock:
+            S = self._fg_s[self.slot]
+            self._S.value = 0 if S is None else S       # an idle slot: the library reports it
+            _check(self._end(*self._eargs))             # (on failure the request stays in flight)
+            self._fg_s[self.slot] = None
+        return self._f[:S].copy(), self._g[:S].copy(), self._low[:S].copy()
+
+
 COMM_ID_BYTES = 128
 
 
@@ -725,4 +785,4 @@ __all__ = ["gen_draw", "gen_assemble", "gen_dates", "LbOptions", "LbResult", "Co
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN", "PATH_FUSED_MT",
            "LIB_PATH",
            "SIGNATURES",
-           "Comm", "comm_id", "best_start", "COMM_ID_BYTES"]
+           "Comm", "comm_id", "best_start", "COMM_ID_BYTES", "FgChannel"]

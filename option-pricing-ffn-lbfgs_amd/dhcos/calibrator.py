@@ -109,24 +109,28 @@ _EXP_MASK = np.zeros(N_PARAMS, dtype=bool)
 _EXP_MASK[_EXP] = True
 
 
-def fd_models(X0, h=FD_ABS_STEP):
+def fd_models(X0, h=FD_ABS_STEP, out=None):
     """[2, S, 13]: the model params (x_to_model) of every x0 row and of x0 + h, h as
     fd_request_points_many forms it.  NumPy's exp / tanh as the reference's transform_params
-    calls them element by element (the same SIMD loops, so the same bits), in three ufunc calls:
-    the per-iteration host cost of the SciPy driver (tests/test_gpu_parity.py holds fg() to
+    calls them element by element (the same SIMD loops, so the same bits), in place in one
+    [2S, 13] array (out: the caller's [2, S, 13] buffer, e.g. _native.FgChannel.model_out): the
+    per-iteration host cost of the SciPy driver (tests/test_gpu_parity.py holds fg() to
     fg_from_losses() bit for bit)."""
     X0 = np.asarray(X0, dtype=np.float64)
-    Xh = X0 + h
+    S = X0.shape[0]
+    P = np.empty((2 * S, N_PARAMS)) if out is None else out.reshape(2 * S, N_PARAMS)
+    P[:S] = X0
+    Xh = P[S:]
+    np.add(X0, h, out=Xh)
     d = Xh - X0
     if np.count_nonzero(d) != d.size:                 # some step vanishes (d == 0); NaN counts
         vanish = d == 0                                # as nonzero, as in (Xh - X0) == 0
         sign = np.where(X0 >= 0, 1.0, -1.0)
-        Xh = X0 + np.where(vanish, _SQRT_EPS * sign * np.maximum(1.0, np.abs(X0)), h)
-    XX = np.concatenate([X0, Xh])
-    P = np.exp(XX, out=XX.copy(), where=_EXP_MASK)      # identity where the mask is off
-    P[:, 4] = np.tanh(XX[:, 4])
-    P[:, 9] = np.tanh(XX[:, 9])
-    return P.reshape(2, X0.shape[0], N_PARAMS)
+        Xh[...] = X0 + np.where(vanish, _SQRT_EPS * sign * np.maximum(1.0, np.abs(X0)), h)
+    np.exp(P, out=P, where=_EXP_MASK)                 # identity where the mask is off
+    np.tanh(P[:, 4], out=P[:, 4])
+    np.tanh(P[:, 9], out=P[:, 9])
+    return P.reshape(2, S, N_PARAMS)
 
 
 def _custom_loss(cal):
@@ -681,6 +685,10 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
     inflight = [None, None]
     busy = [False, False]              # slot k holds a request of this loop (fg_begin .. fg_end)
     launches = 0
+    # the two slots with their arguments prepared once (_native.FgChannel: the per-request host
+    # path is a row copy in, one foreign call each way, three small copies out)
+    chans = [_native.FgChannel(surf, k, max(1, len(groups[k])), cal.spot, cal.risk_free_rate,
+                               cal.N) for k in (0, 1)]
 
     def submit(k):
         ids = [sid for sid in groups[k] if sid in pending]
@@ -689,7 +697,7 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
             return
         X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
         try:
-            model = fd_models(X0)
+            fd_models(X0, out=chans[k].model_out(len(ids)))
         except Exception:          # reference: except -> continue, for the raising start only
             keep = []
             for j, sid in enumerate(ids):
@@ -702,9 +710,9 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
             if not keep:
                 return
             ids, X0 = [ids[j] for j in keep], X0[keep]
-            model = fd_models(X0)
+            fd_models(X0, out=chans[k].model_out(len(ids)))
         cal.loss_evals += X0.shape[0] * (N_PARAMS + 1)
-        surf.fg_begin(X0, cal.spot, cal.risk_free_rate, cal.N, model=model, slot=k)
+        chans[k].begin(X0)
         inflight[k] = ids
         busy[k] = True
 
@@ -719,7 +727,7 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
                 if ids is None:
                     continue
                 inflight[k] = None
-                f0, G, lows = surf.fg_end(k)
+                f0, G, lows = chans[k].end()
                 busy[k] = False
                 launches += 1
                 _consume(states, gens, pending, outcomes, ids, f0, G, lows)
