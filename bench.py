@@ -192,6 +192,8 @@ def cpu_options(cfg):
 
 def kernel_label(ctx):
     """Kernels of the last request on ctx (after the bench's own launches)."""
+    if ctx.last_path == _native.PATH_FUSED_MT:
+        return "cos_fused_mt_kernel (several param sets of one maturity group per block)"
     if ctx.last_path == _native.PATH_FUSED:
         return "cos_fused_kernel (after table_prologue_kernel on grids of >= 8,192 tables)"
     if ctx.last_path == _native.PATH_GEN:
@@ -641,9 +643,10 @@ def main():
                     help="skip the N = 1 side legs of the c3 line (tail cut off, C2 single "
                          "start, C5 generator batch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--path", default="auto", choices=["auto", "split", "fused"],
+    ap.add_argument("--path", default="auto", choices=["auto", "split", "fused", "mt"],
                     help="request kernels (libdhcos dh_ctx_set_path): auto, table+option "
-                         "launches, or one fused launch")
+                         "launches, one fused launch, or one fused launch with several tables "
+                         "per block")
     ap.add_argument("--tail-cut", default="on", choices=["on", "off"],
                     help="adaptive tail of the angle sums (dh_ctx_set_tail_cut; off: every COS "
                          "term summed, for A/B)")
@@ -704,7 +707,8 @@ def main():
             sys.exit(f"bench.py: ranks share GPUs under RCCL: {devs}")
     os.environ["DHCOS_DEVICE"] = str(local)
     _native.default_context().set_path({"auto": _native.PATH_AUTO, "split": _native.PATH_SPLIT,
-                                        "fused": _native.PATH_FUSED}[args.path])
+                                        "fused": _native.PATH_FUSED,
+                                        "mt": _native.PATH_FUSED_MT}[args.path])
     _native.default_context().set_tail_cut(args.tail_cut == "on")
     # a dedicated (non-null) stream: libdhcos launches on it and the HIP events time it
     stream = torch.cuda.Stream(device=dev)

@@ -13,7 +13,7 @@ for rep in 1 2; do
       mt*) unset DHCOS_LIB; export DHCOS_MT_TB=${v#mt} ;;        # mt0 / mt2 / mt4: tables per block
       *) export DHCOS_LIB=$PWD/option-pricing-ffn-lbfgs_amd/dhcos/libdhcos_$v.so ;;
     esac
-    timeout -k 10 120 python3 bench.py --config $CONFIG --no-cpu --no-calib --no-side --steps ${STEPS:-200} --warmup 20 \
+    timeout -k 10 120 python3 bench.py --config $CONFIG --path ${BPATH:-auto} --no-cpu --no-calib --no-side --steps ${STEPS:-200} --warmup 20 \
         > gpurun_out/ab/${CONFIG}_${v}_$rep.json 2> gpurun_out/ab/${CONFIG}_${v}_$rep.err || { echo "$v failed"; tail -3 gpurun_out/ab/${CONFIG}_${v}_$rep.err; exit 1; }
     python3 -c "
 import json,sys; d=json.loads(open('gpurun_out/ab/${CONFIG}_${v}_$rep.json').read().strip().splitlines()[-1])
