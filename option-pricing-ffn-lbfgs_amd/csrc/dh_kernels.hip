@@ -2147,8 +2147,8 @@ constexpr int kMtMaxTB = 4;
 // LDS of one table of the multi-table kernel: (T2, T6)[N] | xK, e^xK, cos/sin step, sse, bad,
 // clamp prices [cap] | lane partials (kRedDoubles, block-wide tiles)
 // (rounded to whole 16-byte pairs: the next table's (T2, T6) are double2)
-__host__ __device__ constexpr int mt_table_doubles(int N, int cap) {
-    return (2 * N + 7 * cap + kRedDoubles + 1) / 2 * 2;
+__host__ __device__ constexpr int mt_table_doubles(int N, int cap, int TT) {
+    return (2 * N + 7 * cap + (TT == kBlock ? kRedDoubles : 0) + 1) / 2 * 2;
 }
 // shared per block: K, mkt [cap] doubles | call, perm [cap] ints, rounded to 16-byte pairs
 __host__ __device__ constexpr int mt_shared_doubles(int cap) { return (3 * cap + 1) / 2 * 2; }
@@ -2158,7 +2158,8 @@ __global__ __launch_bounds__(TB * TT, DH_FUSED_WAVES) void cos_fused_mt_kernel(
     const double* __restrict__ h_prm, const double* __restrict__ h_tsrc,
     const int2* __restrict__ h_groups, const int* __restrict__ h_live, int h_tpp, int h_npb,
     PriceArgs A_) {
-    static_assert(TB >= 2 && TB <= kMtMaxTB && TT == kBlock, "multi-table kernel shape");
+    static_assert(TB >= 2 && TB <= kMtMaxTB && (TT == kBlock || TT == kBlock / 2),
+                  "multi-table kernel shape");
     constexpr int NT = TB * TT;
     constexpr int NW = NT / 64;
     static_assert(NW >= 2 * TB, "one c0 and one c5 wave per table");
@@ -2188,7 +2189,7 @@ __global__ __launch_bounds__(TB * TT, DH_FUSED_WAVES) void cos_fused_mt_kernel(
     int* shPerm = shCall + cap;
     double* tab0 = smem + mt_shared_doubles(cap);
     auto tab_lds = [&](int j, double*& lclp, double*& red) {
-        double* base = tab0 + (size_t)j * mt_table_doubles(N, cap);
+        double* base = tab0 + (size_t)j * mt_table_doubles(N, cap, TT);
         TileLds L;
         L.t26 = (double2*)base;
         L.K = shK;
@@ -2624,8 +2625,11 @@ int table_tpt(const dh_ctx_view& v, int64_t n_q, int N) {
 }
 
 // option-kernel threads per task: enough lanes for ceil(nopt/kR) groups, LDS permitting
+#ifndef DH_BIG_TILE_TPT
+#define DH_BIG_TILE_TPT 256   // option threads of tiles of more than 64 options (128: G <= 4 lanes
+#endif                        // per 4-option group on C3's 100-option tiles)
 int option_tpt(int max_nopt, int N, int cap) {
-    int tpt = max_nopt <= kR ? 64 : (max_nopt <= 4 * kR ? 128 : 256);
+    int tpt = max_nopt <= kR ? 64 : (max_nopt <= 4 * kR ? 128 : (max_nopt > 64 ? DH_BIG_TILE_TPT : 256));
     while (tpt < kBlock &&
            ((size_t)(kBlock / tpt) * option_lds_doubles(N, cap) + (tpt == kBlock ? kRedDoubles : 0)) *
                    sizeof(double) > (size_t)kLdsDyn)
@@ -2751,8 +2755,10 @@ int ensure_attrs(dh_ctx* ctx) {
           (const void*)cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>,
           (const void*)cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>,
           (const void*)cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>,
-          (const void*)cos_fused_mt_kernel<2, kBlock, 1>, (const void*)cos_fused_mt_kernel<2, kBlock, kR>,
-          (const void*)cos_fused_mt_kernel<4, kBlock, 1>, (const void*)cos_fused_mt_kernel<4, kBlock, kR>})
+          (const void*)cos_fused_mt_kernel<2, 256, 1>, (const void*)cos_fused_mt_kernel<2, 256, kR>,
+          (const void*)cos_fused_mt_kernel<4, 256, 1>, (const void*)cos_fused_mt_kernel<4, 256, kR>,
+          (const void*)cos_fused_mt_kernel<2, 128, 1>, (const void*)cos_fused_mt_kernel<2, 128, kR>,
+          (const void*)cos_fused_mt_kernel<4, 128, 1>, (const void*)cos_fused_mt_kernel<4, 128, kR>})
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
@@ -2896,16 +2902,18 @@ int mt_tables_per_block(dh_ctx* ctx) {
     return ctx->mt_tb;
 }
 
-size_t mt_lds_bytes(int TB, int N, int cap) {
-    return ((size_t)mt_shared_doubles(cap) + (size_t)TB * mt_table_doubles(N, cap)) * sizeof(double);
+size_t mt_lds_bytes(int TB, int TT, int N, int cap) {
+    return ((size_t)mt_shared_doubles(cap) + (size_t)TB * mt_table_doubles(N, cap, TT)) *
+           sizeof(double);
 }
 
 // 0 if cos_fused_mt_kernel does not apply to the request, else its tables per block
 int mt_applies(dh_ctx* ctx, const PriceArgs& A0) {
     const int TB = mt_tables_per_block(ctx);
     if (!TB || A0.paired || A0.strike_mode != DH_STRIKE_ABSOLUTE || ctx->stamps_on) return 0;
-    if (A0.max_group > kTileMax || option_tpt(A0.opt_cap, A0.N, A0.opt_cap) != kBlock) return 0;
-    if (mt_lds_bytes(TB, A0.N, A0.opt_cap) > (size_t)kLdsDyn) return 0;
+    const int TT = option_tpt(A0.opt_cap, A0.N, A0.opt_cap);
+    if (A0.max_group > kTileMax || (TT != kBlock && TT != kBlock / 2)) return 0;
+    if (mt_lds_bytes(TB, TT, A0.N, A0.opt_cap) > (size_t)kLdsDyn) return 0;
     return TB;
 }
 
@@ -2917,16 +2925,25 @@ int launch_fused_mt(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st, int TB) {
     PriceArgs A = A0;
     A.p0 = 0;
     A.np = A0.P;
-    const size_t lds = mt_lds_bytes(TB, A.N, A.opt_cap);
-    const bool r1 = tile_r(A.opt_cap, kBlock) == 1;
-    const dim3 grid((unsigned)blocks), block((unsigned)(TB * kBlock));
+    const int TT = option_tpt(A.opt_cap, A.N, A.opt_cap);
+    const size_t lds = mt_lds_bytes(TB, TT, A.N, A.opt_cap);
+    const bool r1 = tile_r(A.opt_cap, TT) == 1;
+    const dim3 grid((unsigned)blocks), block((unsigned)(TB * TT));
     const double* tsrc = A.group_T;
-    switch (TB * (r1 ? 1 : -1)) {
-        case 2: hipLaunchKernelGGL((cos_fused_mt_kernel<2, kBlock, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, tpp, (int)pb, A); break;
-        case -2: hipLaunchKernelGGL((cos_fused_mt_kernel<2, kBlock, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, tpp, (int)pb, A); break;
-        case 4: hipLaunchKernelGGL((cos_fused_mt_kernel<4, kBlock, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, tpp, (int)pb, A); break;
-        default: hipLaunchKernelGGL((cos_fused_mt_kernel<4, kBlock, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, tpp, (int)pb, A); break;
+#define DH_MT_LAUNCH(tb, tt, rt) hipLaunchKernelGGL((cos_fused_mt_kernel<tb, tt, rt>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, tpp, (int)pb, A)
+    const int key = TB * 1000 + TT * (r1 ? 1 : -1);
+    switch (key) {
+        case 2256: DH_MT_LAUNCH(2, 256, 1); break;
+        case 2000 - 256: DH_MT_LAUNCH(2, 256, kR); break;
+        case 4256: DH_MT_LAUNCH(4, 256, 1); break;
+        case 4000 - 256: DH_MT_LAUNCH(4, 256, kR); break;
+        case 2128: DH_MT_LAUNCH(2, 128, 1); break;
+        case 2000 - 128: DH_MT_LAUNCH(2, 128, kR); break;
+        case 4128: DH_MT_LAUNCH(4, 128, 1); break;
+        case 4000 - 128: DH_MT_LAUNCH(4, 128, kR); break;
+        default: return fail(DH_E_ARG, "multi-table kernel shape");
     }
+#undef DH_MT_LAUNCH
     HIP_TRY(hipGetLastError());
     return DH_OK;
 }
