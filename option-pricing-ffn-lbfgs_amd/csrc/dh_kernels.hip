@@ -1199,12 +1199,14 @@ __device__ __forceinline__ void tile_sums_r(const PriceArgs& A, int64_t p, const
             }
             __syncthreads();
             if (pass == 0) DH_STAMP(A, 11);
-            // lane gl of group gi finalises options j = gl, gl + G, ... (< R) of the group
-            if (gvalid) {
-                for (int j = gl; j < R; j += G) {
-                    const int oi = gi * R + j;
-                    if (oi >= nopt || isnan(L.ss[oi])) continue;
-                    const double* rj = red + j * kBlock + (t - gl);
+            // thread t finalises option pass R + t of the pass (one option per thread: the
+            // pass's options on its first lanes, not on lanes gl < R of every group, so fewer
+            // waves issue the finalisation): its group's G lane partials in lane order
+            const int o_end = min(nopt, min(pass + groups_per_pass, ngroups) * R);
+            for (int oi = pass * R + t; active && oi < o_end; oi += tpt) {
+                if (!isnan(L.ss[oi])) {
+                    const int j = oi % R;
+                    const double* rj = red + j * kBlock + (oi / R - pass) * G;
                     double sum = 0.0;
                     for (int l = 0; l < G; ++l) sum += rj[l];
                     const double v = option_sum(C, L.call[oi] != 0, S0, L.K[oi], L.xK[oi],
@@ -1958,7 +1960,13 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP(A, 6);
         DH_STAMP_T(A, 19, 64);
         DH_STAMP_T(A, 20, 192);
+#ifdef DH_PROBE_SKIP_CF
+        // instruction-count probe only (wrong prices): entries as cheap stand-ins
+        table_entries<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double) {
+            const double w = k < kcf - 7 ? scale : 0.0;        // n_eff ~ K_cf - 7, as measured
+#else
         table_entries<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
+#endif
             if (k == 0) {
                 w0s = 0.5 * w;
                 L.t26[0] = make_double2(0.0, 0.0);
@@ -2034,7 +2042,11 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     DH_STAMP(A, 3);
 
     const Consts C{0.0 + red[0][0], 0.0 + red[1][0], 0.0 + red[2][0], 0.0 + red[3][0], a, b, eb, ea};
+#ifndef DH_PROBE_SKIP_SUMS
     if (t < tpt2) tile_sums_r<RT>(A, p, C, S0, disc, gn, G, tpt2, t, true, L, lclp + cap, sct);
+#else
+    if (t < gn) record_price(A, p, L.perm[t], L.mkt[t], t, C.c0 + L.xK[t], L.sse, L.bad);   // probe only
+#endif
     DH_STAMP(A, 4);
     if (A.part_sse) {
         __syncthreads();
@@ -2886,9 +2898,13 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
 
 // The multi-table fused kernel (cos_fused_mt_kernel): tables per block, from $DHCOS_MT_TB (2 or 4;
 // 0 turns it off), default DH_MT_TB; used from DH_MT_MIN_TABLES tables (AUTO) on surfaces with
-// absolute strikes whose option threads are a whole block (the kernel's TT).
+// absolute strikes whose option threads are 128 or 256 per table.  Off by default: measured
+// (tools/gpu_r4_ab.sh) it loses on C3 / C4 with 256-thread tables (2 tables:
+// 60.7 -> 73 us, C4 235 -> 326 us: 512-thread blocks leave half a CU waiting in their serial
+// phases) and gains 3% on C3 only with 128-thread tables (59.2 us), which cost the one-table
+// kernel 6%.  DH_PATH_FUSED_MT still selects it (the same bits as every other path).
 #ifndef DH_MT_TB
-#define DH_MT_TB 2
+#define DH_MT_TB 0
 #endif
 #ifndef DH_MT_MIN_TABLES
 #define DH_MT_MIN_TABLES 2048

@@ -356,9 +356,10 @@ def test_calibrate_seed0(dh, calib_golden, calib_noise):
 def test_calibrate_5x5_surface_in_noise_ensemble(dh, driver):
     """calibrate(300, 3) under np.random.seed(0) on a second market: the 5 x 5 synthetic surface
     of tests/golden/calib_noise_5x5.json (bench.py's construction at N = 128), against the
-    reference algorithm's outcomes under last-bit price noise (12 members; member 0 the
-    reference-exact scalar pricer).  Per start: the x0 the reference draws, the ensemble's
-    message and a loss inside the members' range for that start (x/ 2: 12 members sample a
+    reference algorithm's outcomes under price noise (24 members: 11 at 1e-15, 12 at 1e-13 --
+    the scale of the GPU's own price differences, at which start 2 also ends CONVERGENCE;
+    member 0 the reference-exact scalar pricer).  Per start: the x0 the reference draws, the ensemble's
+    message and a loss inside the members' range for that start (x/ 2: 24 members sample a
     chaotic map); start 0 (the literature guess on the Feller kink) exactly as every member;
     the winner inside the members' band of final losses.  Per-start outcomes are printed beside
     member 0's."""

@@ -23,7 +23,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel",
+KERNELS = ("cos_fused_mt_kernel", "cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel",
            "table_prologue_kernel", "cos_gen_kernel")
 
 
@@ -51,7 +51,9 @@ def main():
     tpath = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     md = [f"# Profile summary {args.tag}", "",
-          "One request = cos_fused_kernel (every maturity group one tile: C1-C4; on grids of "
+          "One request = cos_fused_mt_kernel (round 4: grids of >= 2,048 tables on block-wide "
+          "tiles, C3 / C4: several param sets of one maturity group per block) or "
+          "cos_fused_kernel (every maturity group one tile: C1-C4; on grids of "
           ">= 8,192 blocks, C4, preceded by table_prologue_kernel), cos_gen_kernel (generator "
           "grids, C5: one fused small-tile launch per batch), or cos_table_kernel + the option "
           "kernel (--path split; cos_option_kernel for multi-tile groups, "
