@@ -526,13 +526,19 @@ class FgChannel:
         """The [2, S, 13] model buffer of a request of S starts (fd_models(..., out=))."""
         return self._m[:2 * S * 13].reshape(2, S, 13)
 
+    def x_rows(self, S: int) -> np.ndarray:
+        """The [S, 13] point buffer of a request of S starts: rows written here need no copy
+        in begin()."""
+        return self._x[:S]
+
     def begin(self, X0: np.ndarray, model: np.ndarray = None):
-        """Enqueue the request of X0 [S, 13] (model: [2, S, 13], default: already written into
-        model_out(S))."""
+        """Enqueue the request of X0 [S, 13] (x_rows(S) itself, or rows to copy there; model:
+        [2, S, 13], default: already written into model_out(S))."""
         S = X0.shape[0]
         if S > self.s_max or S < 1:
             raise ValueError(f"request of {S} starts on a channel of {self.s_max}")
-        self._x[:S] = X0
+        if X0.base is not self._x:
+            self._x[:S] = X0
         if model is not None:
             self.model_out(S)[...] = model
         with self._lock:

@@ -519,32 +519,31 @@ class _StartState:
         self.best_loss = np.inf
 
 
-# prices per param set (options x COS terms) below which a request's device time is shorter than
-# the host work a second request group adds per iteration (fd_models, the ctypes calls, the
-# bookkeeping: ~20 us), so one lockstep group is faster than the two-group pipeline (C1: 15 x 128)
-PIPELINE_MIN_PRICES = 16384
-
-
-def _pipeline_surface(cal, n_starts, force=None):
-    """The surface the two-group pipelined loop may use, or None: subclassed losses, markets
-    without a surface, one start, or groups too large for one asynchronous request keep the
-    lockstep loop; so do (force None: automatic, $DHCOS_SCIPY_PIPELINE = 0 / 1 overrides) markets
-    whose requests are too short to hide a group's host work (PIPELINE_MIN_PRICES)."""
-    if force is None:
-        env = os.environ.get("DHCOS_SCIPY_PIPELINE", "")
-        force = {"0": False, "1": True}.get(env)
-    if force is False:
-        return None
-    if n_starts < 2 or -(-n_starts // 2) * (N_PARAMS + 1) > _native_async_max_sets():
+def _native_surface(cal, group_starts):
+    """The surface whose request slots (dh_surface_fg_begin / _end through _native.FgChannel) a
+    loop may drive directly for groups of up to group_starts starts, or None: subclassed losses
+    and fg_batch overrides (their values must be used), markets without a surface, and groups too
+    large for one asynchronous request take the generic _fg path."""
+    if group_starts * (N_PARAMS + 1) > _native_async_max_sets():
         return None
     cls = type(cal)
     if (not isinstance(cal, DoubleHestonJumpCalibrator)
             or cls.fg_batch is not DoubleHestonJumpCalibrator.fg_batch
             or _custom_loss(cal) or not len(cal.market_options)):
         return None
-    if force is None and len(cal.market_options) * getattr(cal, "N", 128) < PIPELINE_MIN_PRICES:
-        return None
     return cal._get_surface()
+
+
+def _pipeline_surface(cal, n_starts, force=None):
+    """The surface the two-group pipelined loop may use, or None: one start, no native channel
+    for half the starts (_native_surface), or force False ($DHCOS_SCIPY_PIPELINE = 0 when force is
+    None) keep the lockstep loop.  Round 4 measured the pipeline ahead on every bench surface once
+    both loops drive prepared slots (C1 calibrate(300, 3) 5.0 vs 5.6 ms, C2 6.0 vs 6.8 ms)."""
+    if force is None:
+        force = {"0": False, "1": True}.get(os.environ.get("DHCOS_SCIPY_PIPELINE", ""))
+    if force is False or n_starts < 2:
+        return None
+    return _native_surface(cal, -(-n_starts // 2))
 
 
 def _native_async_max_sets():
@@ -635,25 +634,52 @@ def _fg_per_start(cal, ids, X0, gens, pending, exc=None):
 
 
 def _advance(cal, gens, states, order, outcomes):
-    """run_starts' loop: one launch per lockstep request, setulb steps per start."""
+    """run_starts' loop: one launch per lockstep request, setulb steps per start.  On a native
+    market the requests go through one prepared request slot (_native.FgChannel on slot 0:
+    zero-copy points in, a spin-wait on the request's event, no per-call argument marshalling),
+    else through cal.fg_batch; both give the same values (fg_batch is dh_surface_fg)."""
     launches = 0
-    for group in order:
-        pending = {}
-        for sid in group:
-            pending[sid] = next(gens[sid])
-        while pending:
-            ids = sorted(pending)
-            X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
+    surf = _native_surface(cal, max(len(g) for g in order)) if order else None
+    chan = None if surf is None else _native.FgChannel(surf, 0, max(len(g) for g in order),
+                                                       cal.spot, cal.risk_free_rate, cal.N)
+    busy = False
+
+    def fg(X0):
+        nonlocal busy
+        if chan is None:
+            return _fg(cal, X0)
+        fd_models(X0, out=chan.model_out(X0.shape[0]))
+        cal.loss_evals += X0.shape[0] * (N_PARAMS + 1)
+        chan.begin(X0)
+        busy = True
+        out = chan.end()
+        busy = False
+        return out
+
+    try:
+        for group in order:
+            pending = {}
+            for sid in group:
+                pending[sid] = next(gens[sid])
+            while pending:
+                ids = sorted(pending)
+                X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
+                try:
+                    f0, G, lows = fg(X0)
+                except _native.NativeError:
+                    raise
+                except Exception as exc:   # some start's loss raised: drop that start only
+                    ids, f0, G, lows = _fg_per_start(cal, ids, X0, gens, pending, exc)
+                    if not ids:
+                        continue
+                launches += 1
+                _consume(states, gens, pending, outcomes, ids, f0, G, lows)
+    finally:
+        if busy:                       # unwinding with the slot's request in flight
             try:
-                f0, G, lows = _fg(cal, X0)
-            except _native.NativeError:
-                raise
-            except Exception as exc:   # some start's loss raised: drop that start only
-                ids, f0, G, lows = _fg_per_start(cal, ids, X0, gens, pending, exc)
-                if not ids:
-                    continue
-            launches += 1
-            _consume(states, gens, pending, outcomes, ids, f0, G, lows)
+                surf.ctx.fg_cancel(0)
+            except Exception:          # noqa: BLE001 -- unwinding: the first error wins
+                pass
     cal.lockstep_launches = launches
 
 
@@ -695,7 +721,9 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
         inflight[k] = None
         if not ids:
             return
-        X0 = np.array([pending[sid] for sid in ids])   # = np.stack, ~3 us sooner
+        X0 = chans[k].x_rows(len(ids))                 # the rows straight into the slot
+        for j, sid in enumerate(ids):
+            X0[j] = pending[sid]
         try:
             fd_models(X0, out=chans[k].model_out(len(ids)))
         except Exception:          # reference: except -> continue, for the raising start only
