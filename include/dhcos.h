@@ -113,6 +113,17 @@ int dh_surface_size(const dh_surface* s, int* M, int* n_tiles);
 int dh_surface_price(dh_ctx* ctx, const dh_surface* s, const double* params, int64_t P, int N,
                      double L, double* out);
 
+/* The generator's pricing from its sampler's columns (synthetic_generator.py:123-138): params
+ * [P][13] model params, spots [P] (each record's S0), one rate r and q = 0 -- the records of
+ * dh_surface_price, formed on the device (no host packing pass), then priced into out[P][M].
+ * Host buffers; registered ones (dh_host_register) move by DMA without staging copies.         */
+int dh_surface_price_cols(dh_ctx* ctx, const dh_surface* s, const double* params,
+                          const double* spots, double r, int64_t P, int N, double L, double* out);
+/* Page-lock a host range for the copies of the calls above (hipHostRegister) and release it.
+ * A range must be unregistered before its memory is freed.                                     */
+int dh_host_register(void* ptr, size_t bytes);
+int dh_host_unregister(void* ptr);
+
 /* Calibration objective over the surface for S param sets (one FD request = 14 sets):
  *   sse[s]   = sum_m ((price_sm - mkt_m) / mkt_m)^2      (lbfgs_calibrator.py:163, un-normalised)
  *   n_bad[s] = #{m : price_sm is NaN, +-inf or <= 0}      (lbfgs_calibrator.py:152)

@@ -468,6 +468,11 @@ struct BitsScratch {
 
 void par_bits(ParDraw& P, int64_t b, BitsScratch& S) {
     static const bool avx2 = __builtin_cpu_supports("avx2");
+    const int64_t t0 = P.block_t0(b), t1 = std::min(P.block_t0(b + 1), P.max_t);
+    if (t1 <= t0) {             // a block past the stream bound (the last of max_blocks): no pairs
+        P.block_done[b].store(1, std::memory_order_release);
+        return;
+    }
     // raw key words of generations 64 b .. 64 b + 64 (the next block's first words close the
     // block's last pairs), tempered in place by the body
     LegacyRng r;
@@ -479,7 +484,6 @@ void par_bits(ParDraw& P, int64_t b, BitsScratch& S) {
         std::memcpy(S.w.data() + (int64_t)gi * kMtN, r.key, sizeof(r.key));
     }
     const int64_t base = b * kBlockWords - P.pos0;          // word n at w[n - base]
-    const int64_t t0 = P.block_t0(b), t1 = std::min(P.block_t0(b + 1), P.max_t);
     const int64_t nd = t1 - t0 + 1;                          // doubles t0 .. t1
     S.d.resize(nd);
     const int64_t q0 = 2 * t0 - base;

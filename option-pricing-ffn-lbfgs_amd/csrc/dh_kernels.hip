@@ -2465,6 +2465,18 @@ __global__ __launch_bounds__(kBlock) void cos_exact_kernel(PriceArgs A, double* 
 }
 
 // Loss sums from a [P][M] price buffer (validation mode): one wave per param set, fixed order.
+// The generator's param records from its sampler's columns (dh_surface_price_cols): rec[i][c] =
+// params[i][c] (c < 13), spots[i], r, 0 -- one thread per record field, coalesced stores.
+__global__ void gen_records_kernel(const double* __restrict__ params,
+                                   const double* __restrict__ spots, double r, int64_t P,
+                                   double* __restrict__ rec) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P * DH_PARAM_STRIDE) return;
+    const int64_t row = i / DH_PARAM_STRIDE;
+    const int c = (int)(i % DH_PARAM_STRIDE);
+    rec[i] = c < 13 ? params[row * 13 + c] : (c == 13 ? spots[row] : (c == 14 ? r : 0.0));
+}
+
 __global__ void loss_from_prices_kernel(const double* __restrict__ prices,
                                         const double* __restrict__ mkt, int M, int64_t S,
                                         double* __restrict__ sse, int* __restrict__ n_bad) {
@@ -3470,6 +3482,50 @@ int dh_surface_price(dh_ctx* ctx, const dh_surface* s, const double* params, int
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(out, ctx->out.ptr, ob, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return DH_OK;
+}
+
+int dh_surface_price_cols(dh_ctx* ctx, const dh_surface* s, const double* params,
+                          const double* spots, double r, int64_t P, int N, double L, double* out) {
+    if (!ctx || !s || (P > 0 && (!params || !spots || !out))) return fail(DH_E_ARG, "null argument");
+    int rc = check_N(N);
+    if (rc) return rc;
+    if (P < 0) return fail(DH_E_ARG, "P < 0");
+    if (P == 0 || s->M == 0) return DH_OK;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.rc) return dev_scope.rc;
+    hipStream_t st = ctx->stream;
+    const size_t ob = (size_t)P * s->M * 8;
+    HIP_TRY(ctx->params.reserve((size_t)P * DH_PARAM_STRIDE * 8));
+    HIP_TRY(ctx->aux0.reserve((size_t)P * 13 * 8));
+    HIP_TRY(ctx->aux1.reserve((size_t)P * 8));
+    HIP_TRY(ctx->out.reserve(ob));
+    HIP_TRY(hipMemcpyAsync(ctx->aux0.ptr, params, (size_t)P * 13 * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->aux1.ptr, spots, (size_t)P * 8, hipMemcpyHostToDevice, st));
+    const int64_t n_el = P * DH_PARAM_STRIDE;
+    const int64_t nb = (n_el + 255) / 256;
+    if (nb > 0x7fffffffLL) return fail(DH_E_ARG, "launch too large");
+    hipLaunchKernelGGL(gen_records_kernel, dim3((unsigned)nb), dim3(256), 0, st,
+                       (const double*)ctx->aux0.ptr, (const double*)ctx->aux1.ptr, r, P,
+                       (double*)ctx->params.ptr);
+    HIP_TRY(hipGetLastError());
+    rc = dh_surface_price_dev(ctx, s, (const double*)ctx->params.ptr, P, N, L,
+                              (double*)ctx->out.ptr, st);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, ctx->out.ptr, ob, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return DH_OK;
+}
+
+int dh_host_register(void* ptr, size_t bytes) {
+    if (!ptr || !bytes) return fail(DH_E_ARG, "null or empty range");
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return DH_OK;
+}
+
+int dh_host_unregister(void* ptr) {
+    if (!ptr) return fail(DH_E_ARG, "null argument");
+    HIP_TRY(hipHostUnregister(ptr));
     return DH_OK;
 }
 

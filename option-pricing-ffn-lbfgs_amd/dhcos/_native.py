@@ -71,6 +71,10 @@ SIGNATURES = {
     "dh_surface_price": (C.c_int, [_vp, _vp, _dp, C.c_int64, C.c_int, C.c_double, _dp]),
     # the per-iteration calibration call takes raw addresses (ndarray.ctypes.data): half the
     # marshalling cost of data_as() pointers
+    "dh_surface_price_cols": (C.c_int, [_vp, _vp, _dp, _dp, C.c_double, C.c_int64, C.c_int,
+                                        C.c_double, _dp]),
+    "dh_host_register": (C.c_int, [_vp, C.c_size_t]),
+    "dh_host_unregister": (C.c_int, [_vp]),
     "dh_surface_loss": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp]),
     "dh_surface_price_dev": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp, _vp]),
     "dh_surface_loss_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp,
@@ -254,6 +258,8 @@ class Context:
                 self._fg_s[int(slot)] = None
 
     def close(self):
+        for surf in self.__dict__.pop("_grid_surfaces", {}).values():   # generator.price_grid's
+            surf.close()
         if getattr(self, "_h", None):
             load().dh_ctx_destroy(self._h)
             self._h = None
@@ -391,13 +397,37 @@ class Surface:
         except Exception:
             pass
 
-    def price(self, params, N=128, L=10.0):
+    def price(self, params, N=128, L=10.0, out=None):
+        """Prices [P, M] of every param row (out: a C-contiguous float64 [P, M] to write into)."""
         params = _f64(params).reshape(-1, PARAM_STRIDE)
         P = params.shape[0]
-        out = np.empty((P, self.M))
+        if out is None:
+            out = np.empty((P, self.M))
+        elif (out.dtype != np.float64 or out.shape != (P, self.M)
+              or not out.flags.c_contiguous or not out.flags.writeable):
+            raise ValueError(f"out must be a writeable C-contiguous float64 [{P}, {self.M}]")
         with self.ctx._lock:
             _check(load().dh_surface_price(self.ctx.handle, self._h, _ptr(params), P, int(N),
                                            float(L), _ptr(out)))
+        return out
+
+    def price_cols(self, params, spots, r, N=128, L=10.0, out=None):
+        """dh_surface_price_cols: prices [P, M] from model params [P, 13] and spots [P] (records
+        formed on the device; out: a C-contiguous float64 [P, M] to write into)."""
+        params = _f64(params).reshape(-1, 13)
+        spots = _f64(spots).reshape(-1)
+        P = params.shape[0]
+        if spots.size != P:
+            raise ValueError("params and spots differ in length")
+        if out is None:
+            out = np.empty((P, self.M))
+        elif (out.dtype != np.float64 or out.shape != (P, self.M)
+              or not out.flags.c_contiguous or not out.flags.writeable):
+            raise ValueError(f"out must be a writeable C-contiguous float64 [{P}, {self.M}]")
+        with self.ctx._lock:
+            _check(load().dh_surface_price_cols(self.ctx.handle, self._h, _ptr(params),
+                                                _ptr(spots), float(r), P, int(N), float(L),
+                                                _ptr(out)))
         return out
 
     def loss_terms(self, params, N=128, L=10.0, want_prices=False):
@@ -773,6 +803,31 @@ def resolve_device(device: int | None = None) -> int:
     return 0
 
 
+class pinned:
+    """Context manager: page-lock the memory of C-contiguous NumPy arrays for its duration
+    (dh_host_register), so the library's copies of them run as DMA without staging.  An array
+    that cannot be registered (e.g. already registered) is left pageable: the copies then stage
+    as usual, with the same results."""
+
+    def __init__(self, *arrays):
+        self._arrays = [a for a in arrays if a is not None and a.nbytes and a.flags.c_contiguous]
+        self._done = []
+
+    def __enter__(self):
+        lib = load()
+        for a in self._arrays:
+            if lib.dh_host_register(a.ctypes.data, a.nbytes) == 0:
+                self._done.append(a)
+        return self
+
+    def __exit__(self, *exc):
+        lib = load()
+        while self._done:
+            a = self._done.pop()
+            lib.dh_host_unregister(a.ctypes.data)
+        return False
+
+
 def default_context(device: int | None = None) -> Context:
     """Per-thread cached context on ``device`` (default: resolve_device())."""
     device = resolve_device(device)
@@ -791,4 +846,4 @@ __all__ = ["gen_draw", "gen_assemble", "gen_dates", "LbOptions", "LbResult", "Co
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN", "PATH_FUSED_MT",
            "LIB_PATH",
            "SIGNATURES",
-           "Comm", "comm_id", "best_start", "COMM_ID_BYTES", "FgChannel"]
+           "Comm", "comm_id", "best_start", "COMM_ID_BYTES", "FgChannel", "pinned"]

@@ -141,23 +141,27 @@ def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES,
     ctx = _native.default_context(device)
     Krel = np.tile(np.asarray(strikes, dtype=np.float64), len(maturities))
     T = np.repeat(np.asarray(maturities, dtype=np.float64), len(strikes))
-    surf = _native.Surface(ctx, Krel, T, np.ones(T.size, dtype=np.int8),
-                           strike_mode=_native.STRIKE_PCT_SPOT)
+    # the grid's surface lives with the context (one per grid): creating and destroying it per
+    # call cost a device allocation and a synchronising free per call
+    grids = ctx.__dict__.setdefault("_grid_surfaces", {})
+    key = (Krel.tobytes(), T.tobytes())
+    surf = grids.get(key)
+    if surf is None:
+        surf = grids[key] = _native.Surface(ctx, Krel, T, np.ones(T.size, dtype=np.int8),
+                                            strike_mode=_native.STRIKE_PCT_SPOT)
     n = params.shape[0]
     out = np.empty((n, T.size))
-    for s in range(0, n, chunk):
-        e = min(n, s + chunk)
-        if ready is not None:
-            ready(e)
-        rec = np.empty((e - s, _native.PARAM_STRIDE))
-        rec[:, :13] = params[s:e]
-        rec[:, 13] = spots[s:e]
-        rec[:, 14] = r
-        rec[:, 15] = 0.0
-        out[s:e] = surf.price(rec, N)
-        if on_chunk is not None:
-            on_chunk(s, e, out)
-    surf.close()
+    params, spots = np.ascontiguousarray(params, dtype=np.float64), np.ascontiguousarray(
+        spots, dtype=np.float64)
+    # the rows move by DMA from / into the page-locked arrays; the device forms the records
+    with _native.pinned(params, spots, out):
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
+            if ready is not None:
+                ready(e)
+            surf.price_cols(params[s:e], spots[s:e], r, N, out=out[s:e])
+            if on_chunk is not None:
+                on_chunk(s, e, out)
     return out
 
 
@@ -169,6 +173,10 @@ def generate_synthetic_calibrations(n_samples: int = 500,
     draw runs on a worker thread and the GPU prices each chunk of samples as soon as the draw has
     finished it (the draw dominates a 1M-sample run, profiles/r03_generator_e2e.json)."""
     d = draw_paths_async(n_samples)
+    dates = []                         # the columnar dates depend on n only: formed meanwhile
+    t_dates = threading.Thread(target=lambda: dates.append(trading_dates_array(n_samples)))
+    if as_arrays:
+        t_dates.start()
     n_opt = d.noise.shape[1]
     Krel = np.tile(STRIKES_PCT, len(MATURITIES))
     asm = (np.empty((n_samples, n_opt)), np.empty(n_samples), np.empty((n_samples, n_opt)))
@@ -188,20 +196,24 @@ def generate_synthetic_calibrations(n_samples: int = 500,
         workers.append(t)
 
     try:
+        # chunks of 65,536 rows (the draw's own): the first is priced as soon as the draw
+        # publishes it, and the last leaves the least pricing after the draw ends
         model = price_grid(d.params, d.spots, N=N, device=device, ready=d.ready,
-                           on_chunk=assemble_rows)
+                           on_chunk=assemble_rows, chunk=1 << 16)
     finally:
         params, spots, noise = d.finish()
         for t in workers:
             t.join()
+        if as_arrays:
+            t_dates.join()
     if errors:
         raise errors[0]
     return assemble(params, spots, noise, model, save_path, as_arrays=as_arrays,
-                    verbose=verbose, N=N, assembled=asm)
+                    verbose=verbose, N=N, assembled=asm, dates=dates[0] if dates else None)
 
 
 def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose=True, N=128,
-             assembled=None):
+             assembled=None, dates=None):
     """Host part after pricing: noise, per-sample loss, output records (:141-183)."""
     say = print if verbose else (lambda *a, **k: None)
     n_samples = params.shape[0]
@@ -211,7 +223,8 @@ def assemble(params, spots, noise, model, save_path, *, as_arrays=False, verbose
     say(f"  samples: {n_samples}   save path: {save_path}   COS terms: {N}")
     # the columnar output keeps the dates as one '<U10' array: 10^6 Python strings were most of
     # the host time of a 1M-sample run (profiles/r03_generator_e2e.json)
-    dates = trading_dates_array(n_samples) if as_arrays else trading_dates(n_samples)
+    if dates is None:
+        dates = trading_dates_array(n_samples) if as_arrays else trading_dates(n_samples)
     names = list(PARAM_RANGES.keys())
     Krel = np.tile(STRIKES_PCT, len(MATURITIES))
     Tg = np.repeat(MATURITIES, len(STRIKES_PCT))

@@ -213,3 +213,17 @@ def test_parallel_draw_equals_numpy_loop(monkeypatch, n_opt, threads, pre):
     for a, b in zip(got, want):
         assert a.shape == b.shape and np.array_equal(a, b)
     assert np.array_equal(after_got, after_want)
+
+
+def test_parallel_draw_small_runs_repeated(monkeypatch):
+    """Draws just above the parallel threshold, repeated: the stream bound's last block lies past
+    the bound (no candidate pairs) and the bit workers may reach it before the walk ends; it must
+    be skipped, not sized negative (a race that aborted the process)."""
+    monkeypatch.setenv("DHCOS_GEN_THREADS", "16")
+    np.random.seed(5)
+    want = G.draw_paths_numpy(4096)
+    for _ in range(60):
+        np.random.seed(5)
+        got = G.draw_paths(4096)
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b)

@@ -578,6 +578,35 @@ def test_generator_pipeline_equals_stages(dh):
     assert np.array_equal(after_got, after_want)
 
 
+def test_price_cols_equals_price_records(dh):
+    """dh_surface_price_cols (the generator's pricing: records formed on the device from the
+    sampler's columns) == dh_surface_price of the host-formed records, bit for bit, from pageable
+    and from page-locked (dh_host_register) arrays, on a chunk that is not a multiple of the
+    record kernel's block."""
+    from dhcos import _native, generator as G
+    np.random.seed(23)
+    n = 70_001
+    p, s, _ = G.draw_paths(n)
+    ctx = _native.default_context()
+    Krel = np.tile(G.STRIKES_PCT, len(G.MATURITIES)).astype(np.float64)
+    T = np.repeat(G.MATURITIES, len(G.STRIKES_PCT)).astype(np.float64)
+    surf = _native.Surface(ctx, Krel, T, np.ones(T.size, dtype=np.int8),
+                           strike_mode=_native.STRIKE_PCT_SPOT)
+    rec = np.zeros((n, _native.PARAM_STRIDE))
+    rec[:, :13], rec[:, 13], rec[:, 14] = p, s, G.RISK_FREE
+    want = surf.price(rec, 128)
+    got = surf.price_cols(p, s, G.RISK_FREE, 128)
+    assert np.array_equal(got, want)
+    out = np.empty_like(want)
+    with _native.pinned(p, s, out):
+        surf.price_cols(p, s, G.RISK_FREE, 128, out=out)
+    assert np.array_equal(out, want)
+    assert surf.price_cols(p[:0], s[:0], G.RISK_FREE, 128).shape == (0, T.size)
+    with pytest.raises(ValueError):
+        surf.price_cols(p, s[:-1], G.RISK_FREE, 128)
+    surf.close()
+
+
 def test_loss_handoff_stress(dh):
     """The fused loss reduction (last-arriver hand-off between workgroups, no fences) checked word
     for word against sums formed on the host from the same kernel's prices, over 300 back-to-back
