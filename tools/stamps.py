@@ -13,8 +13,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["DHCOS_LIB"] = os.path.join(ROOT, "option-pricing-ffn-lbfgs_amd", "dhcos",
-                                       "libdhcos_stamps.so")
+os.environ["DHCOS_LIB"] = os.environ.get("STAMPS_LIB") or os.path.join(
+    ROOT, "option-pricing-ffn-lbfgs_amd", "dhcos", "libdhcos_stamps.so")
 sys.path[:0] = [ROOT, os.path.join(ROOT, "option-pricing-ffn-lbfgs_amd")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
