@@ -51,15 +51,15 @@ def main():
     tpath = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     md = [f"# Profile summary {args.tag}", "",
-          "One request = cos_fused_mt_kernel (round 4: grids of >= 2,048 tables on block-wide "
-          "tiles, C3 / C4: several param sets of one maturity group per block) or "
-          "cos_fused_kernel (every maturity group one tile: C1-C4; on grids of "
+          "One request = cos_fused_kernel (every maturity group one tile: C1-C4; on grids of "
           ">= 8,192 blocks, C4, preceded by table_prologue_kernel), cos_gen_kernel (generator "
           "grids, C5: one fused small-tile launch per batch), or cos_table_kernel + the option "
           "kernel (--path split; cos_option_kernel for multi-tile groups, "
           "cos_option_small_kernel for large calls on <=16-option tiles). Durations: "
           "rocprofv3 --kernel-trace --stats average; counters: per-launch medians of separate "
-          "--pmc passes.", ""]
+          "--pmc passes.  (cos_fused_mt_kernel, several param sets of one maturity group per "
+          "block, runs only under dh_ctx_set_path(PATH_FUSED_MT) / $DHCOS_MT_TB: measured "
+          "slower in round 4.)", ""]
     for c in args.configs.split(","):
         stats = os.path.join(args.src, f"{args.tag}_{c}_stats_kernel_stats.csv")
         if not os.path.exists(stats):
