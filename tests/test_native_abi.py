@@ -109,3 +109,21 @@ def test_comm_and_async_fg_arguments_are_rejected():
     assert lib.dh_surface_fg_end(None, None, 0, 0, None, None, None) == -1
     assert lib.dh_surface_fg_cancel(None, 0) == -1
     assert b"null" in lib.dh_last_error()
+
+
+def test_price_cols_and_host_register_arguments_are_rejected():
+    """dh_surface_price_cols and the page-locking pair validate their arguments before any device
+    work; _native.pinned leaves an array it cannot register pageable (no device here) and never
+    raises for it."""
+    from dhcos import _native
+    lib = _native.load()
+    assert lib.dh_surface_price_cols(None, None, None, None, 0.03, 1, 128, 10.0, None) == -1
+    assert b"null" in lib.dh_last_error()
+    assert lib.dh_host_register(None, 64) == -1
+    assert lib.dh_host_unregister(None) == -1
+    a = np.ones(1000)
+    with _native.pinned(a, None, np.empty(0)) as pin:
+        if _native.device_count() == 0:
+            assert pin._done == []                    # registration failed: left pageable
+        a *= 2.0
+    assert pin._done == [] and a[0] == 2.0            # whatever was registered is released
