@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 from oracle import dh_oracle as O  # noqa: E402
 
 
-def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05):
+def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05, N=128):
     mk = np.array([o["price"] for o in market])
     K = [o["strike"] for o in market]
     T = [o["maturity"] for o in market]
@@ -44,7 +44,7 @@ def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05):
 
     def loss(x):
         p = O.to_params(x)
-        pr = O.price_many(p, S0, K, T, r, call, 128, scalar=scalar)
+        pr = O.price_many(p, S0, K, T, r, call, N, scalar=scalar)
         if eps:
             pr = pr * (1 + eps * rs.uniform(-1, 1, pr.size))
         if not np.all(np.isfinite(pr)) or np.any(pr <= 0):

@@ -394,6 +394,33 @@ def test_calibrate_5x5_surface_in_noise_ensemble(dh, driver):
     assert res.final_loss == min(rr.fun for rr, _ in runs)
 
 
+@pytest.mark.parametrize("driver", ["scipy", "device"])
+def test_calibrate_c2_single_start_matches_reference_algorithm(dh, driver):
+    """configs[1] as BASELINE.json states it: calibrate(300, 1) on the bench's 1,024-option C2
+    surface at N = 256 (tests/golden/calib_c2_single_start.json, the market priced by the oracle)
+    against the reference algorithm's run (oracle losses, SciPy's L-BFGS-B; members 1.. with 1e-13
+    price noise): the same start, the same outcome (message, iterations, evaluations) as every
+    member, and the loss within the loss tolerance of the noise-free member's."""
+    import json
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "calib_c2_single_start.json")) as fh:
+        g = json.load(fh)
+    mkt, S0, r, N = g["market"], g["S0"], g["r"], g["N"]
+    np.random.seed(0)
+    cal = dh.DoubleHestonJumpCalibrator(S0, r, mkt, N=N)
+    assert np.array_equal(cal.start_points(1)[0], np.array(g["x0"]))
+    np.random.seed(0)
+    res = dh.DoubleHestonJumpCalibrator(S0, r, mkt, N=N).calibrate(maxiter=300, multi_start=1,
+                                                                    driver=driver)
+    want = g["members"][0]
+    print(f"{driver}: nit {res.iterations} {res.message!r} loss {res.final_loss:.12e}; reference "
+          f"algorithm: nit {want['nit']} {want['message']!r} loss {want['fun']:.12e}")
+    assert {m["message"] for m in g["members"]} == {want["message"]}
+    assert {m["nit"] for m in g["members"]} == {want["nit"]}
+    assert res.message == want["message"] and res.iterations == want["nit"]
+    assert rel_close(res.final_loss, want["fun"], LOSS_RTOL, 0), (res.final_loss, want["fun"])
+
+
 def test_robust_start_matches_reference_exactly(dh, calib_golden):
     """Start 0 (literature guess on the Feller kink): ABNORMAL after 21 requests, nit 0 (Q12)."""
     from dhcos.calibrator import run_starts
