@@ -69,12 +69,12 @@ SIGNATURES = {
     "dh_surface_destroy": (C.c_int, [_vp]),
     "dh_surface_size": (C.c_int, [_vp, _i32p, _i32p]),
     "dh_surface_price": (C.c_int, [_vp, _vp, _dp, C.c_int64, C.c_int, C.c_double, _dp]),
-    # the per-iteration calibration call takes raw addresses (ndarray.ctypes.data): half the
-    # marshalling cost of data_as() pointers
     "dh_surface_price_cols": (C.c_int, [_vp, _vp, _dp, _dp, C.c_double, C.c_int64, C.c_int,
                                         C.c_double, _dp]),
     "dh_host_register": (C.c_int, [_vp, C.c_size_t]),
     "dh_host_unregister": (C.c_int, [_vp]),
+    # the per-iteration calibration call takes raw addresses (ndarray.ctypes.data): half the
+    # marshalling cost of data_as() pointers
     "dh_surface_loss": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp]),
     "dh_surface_price_dev": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_double, _vp, _vp]),
     "dh_surface_loss_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp,
@@ -567,8 +567,8 @@ class FgChannel:
         S = X0.shape[0]
         if S > self.s_max or S < 1:
             raise ValueError(f"request of {S} starts on a channel of {self.s_max}")
-        if X0.base is not self._x:
-            self._x[:S] = X0
+        if not (X0.base is self._x and X0.ctypes.data == self._x.ctypes.data):
+            self._x[:S] = X0                            # (x_rows(S) itself needs no copy)
         if model is not None:
             self.model_out(S)[...] = model
         with self._lock:
