@@ -158,8 +158,14 @@ def cpu_baseline(cal_opts, S0, r, N, budget_s=12.0, cores=None):
     if cores == 1:
         res = [_cpu_worker(jobs[0])]
     else:
-        with mp.get_context("fork").Pool(cores) as pool:
+        # close + join (not the context manager's terminate()): the workers exit on their own,
+        # so a profiled bench run carries no SIGTERM abort traces of them
+        pool = mp.get_context("fork").Pool(cores)
+        try:
             res = pool.map(_cpu_worker, jobs)
+        finally:
+            pool.close()
+            pool.join()
     n = sum(c for c, _ in res)
     rate = sum(c / t for c, t in res)
     wall = max(t for _, t in res)
@@ -192,8 +198,6 @@ def cpu_options(cfg):
 
 def kernel_label(ctx):
     """Kernels of the last request on ctx (after the bench's own launches)."""
-    if ctx.last_path == _native.PATH_FUSED_MT:
-        return "cos_fused_mt_kernel (several param sets of one maturity group per block)"
     if ctx.last_path == _native.PATH_FUSED:
         return "cos_fused_kernel (after table_prologue_kernel on grids of >= 8,192 tables)"
     if ctx.last_path == _native.PATH_GEN:
@@ -645,10 +649,9 @@ def main():
                     help="skip the N = 1 side legs of the c3 line (tail cut off, C2 single "
                          "start, C5 generator batch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--path", default="auto", choices=["auto", "split", "fused", "mt"],
+    ap.add_argument("--path", default="auto", choices=["auto", "split", "fused"],
                     help="request kernels (libdhcos dh_ctx_set_path): auto, table+option "
-                         "launches, one fused launch, or one fused launch with several tables "
-                         "per block")
+                         "launches, or one fused launch")
     ap.add_argument("--tail-cut", default="on", choices=["on", "off"],
                     help="adaptive tail of the angle sums (dh_ctx_set_tail_cut; off: every COS "
                          "term summed, for A/B)")
@@ -709,8 +712,7 @@ def main():
             sys.exit(f"bench.py: ranks share GPUs under RCCL: {devs}")
     os.environ["DHCOS_DEVICE"] = str(local)
     _native.default_context().set_path({"auto": _native.PATH_AUTO, "split": _native.PATH_SPLIT,
-                                        "fused": _native.PATH_FUSED,
-                                        "mt": _native.PATH_FUSED_MT}[args.path])
+                                        "fused": _native.PATH_FUSED}[args.path])
     _native.default_context().set_tail_cut(args.tail_cut == "on")
     # a dedicated (non-null) stream: libdhcos launches on it and the HIP events time it
     stream = torch.cuda.Stream(device=dev)

@@ -78,11 +78,7 @@ int dh_ctx_set_tail_cut(dh_ctx* ctx, int on);
  * grids: a COS-table launch then the lane-per-option-group kernel); otherwise the table launch
  * then an option launch.  FUSED / SPLIT force one of the two where it applies.  Both produce
  * the same bits; the choice only changes speed.                                              */
-enum { DH_PATH_AUTO = 0, DH_PATH_SPLIT = 1, DH_PATH_FUSED = 2, DH_PATH_GEN = 3, DH_PATH_FUSED_MT = 4 };
-/* DH_PATH_FUSED_MT (round 4): the fused launch with several tables (param sets of one maturity
- * group) per block, their prologues, option staging and CF entries shared out over the block;
- * the same bits as FUSED / SPLIT.  AUTO does not take it by default (measured slower on the
- * bench surfaces; $DHCOS_MT_TB = 2 or 4 enables it from 2,048 tables: DESIGN.md 3.4c).        */
+enum { DH_PATH_AUTO = 0, DH_PATH_SPLIT = 1, DH_PATH_FUSED = 2, DH_PATH_GEN = 3 };
 int dh_ctx_set_path(dh_ctx* ctx, int path);
 /* DH_PATH_FUSED, DH_PATH_SPLIT or DH_PATH_GEN (AUTO only: generator grids -- every maturity group
  * one tile of <= 16 options in a call of >= 65,536 tasks -- priced by one fused small-tile

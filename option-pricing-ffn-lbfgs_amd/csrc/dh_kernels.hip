@@ -1960,13 +1960,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP(A, 6);
         DH_STAMP_T(A, 19, 64);
         DH_STAMP_T(A, 20, 192);
-#ifdef DH_PROBE_SKIP_CF
-        // instruction-count probe only (wrong prices): entries as cheap stand-ins
-        table_entries<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double) {
-            const double w = k < kcf - 7 ? scale : 0.0;        // n_eff ~ K_cf - 7, as measured
-#else
         table_entries<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
-#endif
             if (k == 0) {
                 w0s = 0.5 * w;
                 L.t26[0] = make_double2(0.0, 0.0);
@@ -2042,11 +2036,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     DH_STAMP(A, 3);
 
     const Consts C{0.0 + red[0][0], 0.0 + red[1][0], 0.0 + red[2][0], 0.0 + red[3][0], a, b, eb, ea};
-#ifndef DH_PROBE_SKIP_SUMS
     if (t < tpt2) tile_sums_r<RT>(A, p, C, S0, disc, gn, G, tpt2, t, true, L, lclp + cap, sct);
-#else
-    if (t < gn) record_price(A, p, L.perm[t], L.mkt[t], t, C.c0 + L.xK[t], L.sse, L.bad);   // probe only
-#endif
     DH_STAMP(A, 4);
     if (A.part_sse) {
         __syncthreads();
@@ -2057,359 +2047,6 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     }
     DH_STAMP(A, 5);
     DH_RT_END(A);
-}
-
-// ----------------------------------------------------------------------------------------------
-// multi-table fused request kernel (round 4): one block per TB tables (p, g) .. (p + TB - 1, g) of
-// one maturity group, each table on its own TT threads (TT = the surface's option threads, so the
-// same lane groups G and the same bits as cos_fused_kernel / the split path).  What a table of
-// cos_fused_kernel spends on few lanes is done for the TB tables at once:
-//   * the prologue: wave 0 runs TB tables' prologues lane-parallel, 16 lanes per table (the
-//     factors on alternate lanes, the exponentials one per lane, table_prologue_wave's
-//     expressions), instead of one wave per table on ~6 lanes;
-//   * the option staging: strikes, market prices, types and caller indices once per group;
-//   * the CF entries of the TB tables packed onto the block's threads (C3: 2 x ~140 entries on
-//     512 threads = 5 waves' issue instead of 2 x 3).
-// The CF-cut test keeps one wave per table (its 64 candidates: the first passing one is every
-// path's K_cf), the k-sums the canonical 64-lane order per table, the loss hand-off per (p, tile).
-// ----------------------------------------------------------------------------------------------
-// a wave-uniform double as a scalar value (readfirstlane of both halves)
-__device__ __forceinline__ double uniform_d(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)b);
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-// value of lane (lane & ~15) | l: the lane's 16-lane table group's broadcast
-__device__ __forceinline__ double grp_bcast(double v, int l) {
-    const int src = ((int)__lane_id() & ~15) | l;
-    const long long b = __double_as_longlong(v);
-    const int lo = __shfl((int)b, src, 64);
-    const int hi = __shfl((int)(b >> 32), src, 64);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-// table_prologue_wave for the table of this lane's 16-lane group (sub = lane & 15): the same
-// expressions on the same operands (uncontracted), broadcast within the group; sub-lane 0 writes
-// c[0 .. 30) (K_cf is the cut wave's)
-__device__ __forceinline__ void table_prologue_grp(const PriceArgs& A, const FusedHead& H,
-                                                   int64_t q, double* c, int sub) {
-#pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
-    const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
-    const int g = (int)((unsigned)q % (unsigned)H.tpp);
-    const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
-    const double T = H.tsrc[H.paired ? p : g];
-    const bool two = sub & 1;                      // factor 2 on odd sub-lanes
-    const double v0 = two ? P.v02 : P.v01, k = two ? P.k2 : P.k1, th = two ? P.t2 : P.t1;
-    const double sg = two ? P.s2 : P.s1, rh = two ? P.r2 : P.r1;
-    double c1j, c2j;
-    dh::factor_cumulants(T, P.r, v0, k, th, sg, rh, c1j, c2j);   // double_heston.py:101-118
-    const double c1 = grp_bcast(c1j, 0) + grp_bcast(c1j, 1) + P.lam * T * P.muj;
-    const double c2 = grp_bcast(c2j, 0) + grp_bcast(c2j, 1) +
-                      P.lam * T * (P.sj * P.sj + P.muj * P.muj);
-    const double h = A.L * sqrt(fabs(c2));
-    const double a = c1 - h;                       // trunc_unclamped (double_heston.py:120-132)
-    const double b = c1 + h;
-    int2 gr = make_int2((int)p, 1);
-    if (!H.paired) gr = H.groups[g];
-    const dh::FactorC Fj = dh::factor_consts(v0, k, th, sg, rh);
-    const int e_lane = sub < 6 ? sub : 0;
-    const double arg = e_lane == 0 ? b : e_lane == 1 ? a : e_lane == 2 ? a + 0.1
-                     : e_lane == 3 ? b - 0.1 : e_lane == 4 ? P.muj + 0.5 * (P.sj * P.sj)
-                     : -P.r * T;
-    const double e = exp(arg);
-    dh::CfConsts CC;
-    double* f1 = (double*)&CC.f1;
-    double* f2 = (double*)&CC.f2;
-    const double* fj = (const double*)&Fj;
-    for (int i = 0; i < (int)(sizeof(dh::FactorC) / 8); ++i) {
-        f1[i] = grp_bcast(fj[i], 0);
-        f2[i] = grp_bcast(fj[i], 1);
-    }
-    const double comp = grp_bcast(e, 4) - 1.0;     // cf_consts
-    CC.drift = (P.r - P.q - P.lam * comp) * T;
-    CC.half_sj2 = 0.5 * (P.sj * P.sj);
-    CC.muj = P.muj;
-    CC.lt = P.lam * T;
-    const double e1 = grp_bcast(e, 1), e2 = grp_bcast(e, 2), e3 = grp_bcast(e, 3);
-    const double e5 = grp_bcast(e, 5);
-    if (sub == 0) {
-        c[0] = a;
-        c[1] = b;
-        c[2] = e;
-        c[3] = e1;
-        c[4] = 2.0 / (b - a);
-        c[5] = dh::kPi / (b - a);
-        const double* cc = (const double*)&CC;
-        for (int i = 0; i < 16; ++i) c[6 + i] = cc[i];
-        c[22] = P.S0;
-        c[23] = P.r;
-        c[24] = T;
-        c[25] = e2 * (1.0 + kClampMargin);
-        c[26] = e3 * (1.0 - kClampMargin);
-        c[27] = gr.x;
-        c[28] = gr.y;
-        c[29] = e5;
-    }
-}
-
-constexpr int kMtMaxTB = 4;
-
-// LDS of one table of the multi-table kernel: (T2, T6)[N] | xK, e^xK, cos/sin step, sse, bad,
-// clamp prices [cap] | lane partials (kRedDoubles, block-wide tiles)
-// (rounded to whole 16-byte pairs: the next table's (T2, T6) are double2)
-__host__ __device__ constexpr int mt_table_doubles(int N, int cap, int TT) {
-    return (2 * N + 7 * cap + (TT == kBlock ? kRedDoubles : 0) + 1) / 2 * 2;
-}
-// shared per block: K, mkt [cap] doubles | call, perm [cap] ints, rounded to 16-byte pairs
-__host__ __device__ constexpr int mt_shared_doubles(int cap) { return (3 * cap + 1) / 2 * 2; }
-
-template <int TB, int TT, int RT>
-__global__ __launch_bounds__(TB * TT, DH_FUSED_WAVES) void cos_fused_mt_kernel(
-    const double* __restrict__ h_prm, const double* __restrict__ h_tsrc,
-    const int2* __restrict__ h_groups, const int* __restrict__ h_live, int h_tpp, int h_npb,
-    PriceArgs A_) {
-    static_assert(TB >= 2 && TB <= kMtMaxTB && (TT == kBlock || TT == kBlock / 2),
-                  "multi-table kernel shape");
-    constexpr int NT = TB * TT;
-    constexpr int NW = NT / 64;
-    static_assert(NW >= 2 * TB, "one c0 and one c5 wave per table");
-    const FusedHead H{h_prm, h_tsrc, h_groups, h_live ? h_live : &kLiveOne, nullptr, h_tpp, 0};
-    const PriceArgs& A = A_;
-    const int live_v = *(const __attribute__((address_space(1))) int*)H.live;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    __shared__ double shc[TB][kTabC];
-    __shared__ double kred[TB][4];
-    __shared__ double2 sct[dh::kMathTab];
-    __shared__ unsigned long long cmask[TB][kTileMax / 64];
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int wv = t >> 6;
-    const int g = (int)(blockIdx.x % (unsigned)H.tpp);
-    const int64_t p0 = (int64_t)(blockIdx.x / (unsigned)H.tpp) * TB;
-    const int ntab = (int)min<int64_t>(TB, A.np - p0);     // tables of this block (>= 1)
-    const int N = A.N;
-    const int cap = A.opt_cap;
-    const int2 gr = H.groups[g];
-    const int g0 = gr.x, gn = gr.y;
-
-    // LDS views: shared option arrays, then TB tables
-    double* shK = smem;
-    double* shM = shK + cap;
-    int* shCall = (int*)(shM + cap);
-    int* shPerm = shCall + cap;
-    double* tab0 = smem + mt_shared_doubles(cap);
-    auto tab_lds = [&](int j, double*& lclp, double*& red) {
-        double* base = tab0 + (size_t)j * mt_table_doubles(N, cap, TT);
-        TileLds L;
-        L.t26 = (double2*)base;
-        L.K = shK;
-        L.mkt = shM;
-        L.call = shCall;
-        L.perm = shPerm;
-        L.xK = base + 2 * N;
-        L.exK = L.xK + cap;
-        L.cs = L.exK + cap;
-        L.ss = L.cs + cap;
-        L.sse = L.ss + cap;
-        L.bad = L.sse + cap;
-        lclp = L.bad + cap;
-        red = lclp + cap;
-        return L;
-    };
-
-    // ---- prologue: wave 0, 16 lanes per table || the CF-cut test of table j on wave NW-1-j ||
-    //      option staging on the other waves (and on these after their phase) ----
-    const bool cut_w = wv >= NW - TB;
-    const int cut_j = NW - 1 - wv;
-    if (wv == 0 || cut_w) serial_prio(true);
-    if (wv == 0) {
-        const int j = lane >> 4;
-        if (j < ntab) table_prologue_grp(A, H, (p0 + j) * H.tpp + g, shc[j], lane & 15);
-    } else if (cut_w && cut_j < ntab) {
-        const int kcf = N < kCfCutMinN ? N : prologue_cut_wave(A, H, (p0 + cut_j) * H.tpp + g, lane);
-        if (lane == 0) shc[cut_j][30] = kcf;
-    }
-    dh::load_math_tables(sct, 64);
-    for (int i = (t + NT - 64) % NT; i < gn; i += NT) {       // wave 0 takes the last indices
-        const int m = g0 + i;
-        shK[i] = A.K[m];                                     // the strike mode is applied below
-        shM[i] = A.mkt ? A.mkt[m] : 0.0;
-        shCall[i] = A.call[m];
-        shPerm[i] = A.perm[m];
-    }
-    for (int i = (t + NT - 64) % NT; i < TB * gn; i += NT) {  // per table: its spot's log-strike
-        const int j = i / gn, o = i % gn;
-        if (j >= ntab) continue;
-        const double S0 = H.prm[(p0 + j) * DH_PARAM_STRIDE + 13];
-        double* lclp;
-        double* red;
-        const TileLds L = tab_lds(j, lclp, red);
-        const double K = option_strike(A, g0 + o, S0);
-        double ratio;
-        L.xK[o] = option_logk(K, S0, ratio);            // absolute strikes only (launch_fused_mt)
-        L.exK[o] = ratio;
-    }
-    __syncthreads();
-    serial_prio(false);
-    if (__builtin_amdgcn_readfirstlane(live_v) <= 0) return;
-
-    // ---- clamp-widened options, per (table, 64-option word): masks, then (rare) pricing ----
-    for (int task = wv; task < TB * ((gn + 63) / 64); task += NW) {
-        const int j = task / ((gn + 63) / 64), base = (task % ((gn + 63) / 64)) * 64;
-        if (j >= ntab) continue;
-        double* lclp;
-        double* red;
-        const TileLds L = tab_lds(j, lclp, red);
-        const double a = shc[j][0], b = shc[j][1], T = shc[j][24];
-        const int o = base + lane;
-        bool cl = false;
-        if (o < gn) {
-            const double xK = L.xK[o];
-            cl = xK - 0.1 < a || xK + 0.1 > b;
-        }
-        unsigned long long mask = __ballot(cl);
-        if (lane == 0) cmask[j][base / 64] = mask;
-        if (__builtin_expect(mask != 0, 0)) {
-            const double* prm = H.prm + (p0 + j) * DH_PARAM_STRIDE;
-            const Params P = dh::load_params(prm);
-            const double disc = exp(-P.r * T);
-            while (mask) {
-                const int l = __ffsll((long long)mask) - 1;
-                mask &= mask - 1;
-                const double x = L.xK[base + l];
-                const double ac = (x - 0.1 < a) ? x - 0.1 : a;      // Python min/max
-                const double bc = (x + 0.1 > b) ? x + 0.1 : b;
-                double v = clamped_term_sum(P, T, L.K[base + l], x, ac, bc, L.call[base + l] != 0,
-                                            lane, 64, N, sct);
-                v = xor_sum(v, 64);
-                if (lane == 0) lclp[base + l] = disc * v;
-            }
-        }
-    }
-
-    // ---- CF entries of the TB tables packed on the block's threads ----
-    {
-        int kc[TB], off[TB + 1];
-        off[0] = 0;
-#pragma unroll
-        for (int j = 0; j < TB; ++j) {
-            kc[j] = j < ntab ? (int)shc[j][30] : 0;
-            off[j + 1] = off[j] + kc[j];
-        }
-        int jc = -1;
-        dh::CfConsts CC;
-        double piba = 0.0, a = 0.0, scale = 0.0, T = 0.0, S0 = 0.0;
-        double2* t26 = nullptr;
-        for (int e = t; e < off[TB]; e += NT) {
-            int j = 0;
-#pragma unroll
-            for (int i = 1; i < TB; ++i) j += e >= off[i] ? 1 : 0;
-            if (j != jc) {
-                jc = j;
-                double* cc = (double*)&CC;
-                for (int i = 0; i < 16; ++i) cc[i] = shc[j][6 + i];
-                a = shc[j][0];
-                scale = shc[j][4];
-                piba = shc[j][5];
-                S0 = shc[j][22];
-                T = shc[j][24];
-                double* lclp;
-                double* red;
-                t26 = tab_lds(j, lclp, red).t26;
-            }
-            const int k = e - off[j];
-            const double u = k * piba;                               // table_entries' expressions
-            const double w = dh::cf_phase_re(CC, u, T, a, sct) * scale;
-            if (k == 0) {
-                kred[j][3] = 0.5 * w;
-                t26[0] = make_double2(0.0, 0.0);
-            } else {
-                const double T2 = w * S0 * dh::drcp(1.0 + u * u);
-                t26[k] = make_double2(T2, -(T2 * dh::drcp(u)));
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- k-sums per table in the canonical 64-lane order (c0 + n_eff on wave 2j, c5 on wave
-    //      2j + 1) || per-(table, option) rotations and clamped prices ----
-    if (wv < 2 * TB && (wv >> 1) < ntab) {
-        serial_prio(true);
-        const int j = wv >> 1;
-        const bool f0 = (wv & 1) == 0;
-        double* lclp;
-        double* red;
-        const TileLds L = tab_lds(j, lclp, red);
-        const double a = shc[j][0], b = shc[j][1], eb = shc[j][2], ea = shc[j][3];
-        const double S0 = shc[j][22];
-        const int kcf = (int)shc[j][30];
-        const double delta = tail_delta(A.tail, S0, b - a, N);
-        double c0 = 0.0, c5 = 0.0;
-        int ne = 0;
-        for (int k = lane; k < kcf; k += 64) {
-            if (k == 0) continue;
-            const double T2 = L.t26[k].x;
-            const double cb = (k & 1) ? -1.0 : 1.0;
-            if (f0) {
-                c0 += T2 * eb * cb;
-                ne = max(ne, tail_keep(k, T2, delta));
-            } else {
-                c5 += T2 * ea;
-            }
-        }
-        if (f0) {
-            c0 = xor_sum(c0, 64);
-            ne = xor_max_i(ne, 64);
-            if (lane == 0) {
-                kred[j][0] = c0;
-                kred[j][1] = (double)ne;
-            }
-        } else {
-            c5 = xor_sum(c5, 64);
-            if (lane == 0) kred[j][2] = c5;
-        }
-    }
-    const int G = group_lanes<RT>(gn, N, TT);
-    for (int i = (t + NT - 64 * 2 * TB) % NT; i < TB * gn; i += NT) {   // k-sum waves last
-        const int j = i / gn, o = i % gn;
-        if (j >= ntab) continue;
-        double* lclp;
-        double* red;
-        const TileLds L = tab_lds(j, lclp, red);
-        const double a = shc[j][0], b = shc[j][1];
-        const double ustep = G * dh::kPi / (b - a);
-        const bool cl = (cmask[j][o >> 6] >> (o & 63)) & 1ull;
-        double ss, cs;
-        dh::dsincos(ustep * (cl ? 0.0 : L.xK[o] - a), &ss, &cs);
-        L.cs[o] = cs;
-        L.ss[o] = cl ? NAN : (ss == ss ? ss : 0.0);   // as cos_option_kernel
-        if (cl) record_price(A, p0 + j, L.perm[o], L.mkt[o], o, lclp[o], L.sse, L.bad);
-    }
-    __syncthreads();
-    serial_prio(false);
-
-    // ---- angle sums, finalisation and loss hand-off: table j on threads [j TT, (j + 1) TT) ----
-    const int j = __builtin_amdgcn_readfirstlane(t / TT), ts = t % TT;   // wave-uniform (TT % 64 == 0)
-    const bool valid = j < ntab;
-    double* lclp;
-    double* red;
-    const TileLds L = tab_lds(j < TB ? j : 0, lclp, red);
-    // a table slot past the request's last param set sums nothing (n_eff 0) and records nothing;
-    // the table's constants are wave-uniform: held in SGPRs (the angle sums' VGPR budget)
-    auto U = [&](int i) { return valid ? uniform_d(shc[j][i]) : 0.0; };
-    auto UR = [&](int i) { return valid ? uniform_d(0.0 + kred[j][i]) : 0.0; };
-    const double a = U(0), b = valid ? uniform_d(shc[j][1]) : 1.0;
-    const Consts C{UR(0), UR(1), UR(2), UR(3), a, b, U(2), U(3)};
-    tile_sums_r<RT>(A, p0 + j, C, U(22), U(29), gn, G, TT, ts, valid, L, red, sct);
-    if (A.part_sse) {
-        __syncthreads();
-        if (valid && ts < 64) {
-            serial_prio(true);
-            task_loss(A, p0 + j, (p0 + j) * A.n_tiles + g, gn, ts, L.sse, L.bad);
-        }
-    }
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -2695,7 +2332,6 @@ struct dh_ctx {
     int exact = 0;          // validation mode: every option through the per-term exact path
     int tail_cut = 1;       // adaptive tail of the angle sums (tail_delta; dh_ctx_set_tail_cut)
     int path = DH_PATH_AUTO;   // fused / split request kernels (dh_ctx_set_path)
-    int mt_tb = -1;            // tables per block of cos_fused_mt_kernel (-1: not read yet)
     int last_path = 0;         // kernels of the last fast-path request (dh_ctx_last_path)
     int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
     DevBuf stamps;
@@ -2778,11 +2414,7 @@ int ensure_attrs(dh_ctx* ctx) {
           (const void*)cos_fused_kernel<128, kR>, (const void*)cos_fused_kernel<256, kR>,
           (const void*)cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>,
           (const void*)cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>,
-          (const void*)cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>,
-          (const void*)cos_fused_mt_kernel<2, 256, 1>, (const void*)cos_fused_mt_kernel<2, 256, kR>,
-          (const void*)cos_fused_mt_kernel<4, 256, 1>, (const void*)cos_fused_mt_kernel<4, 256, kR>,
-          (const void*)cos_fused_mt_kernel<2, 128, 1>, (const void*)cos_fused_mt_kernel<2, 128, kR>,
-          (const void*)cos_fused_mt_kernel<4, 128, 1>, (const void*)cos_fused_mt_kernel<4, 128, kR>})
+          (const void*)cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>})
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
@@ -2908,74 +2540,6 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     return DH_OK;
 }
 
-// The multi-table fused kernel (cos_fused_mt_kernel): tables per block, from $DHCOS_MT_TB (2 or 4;
-// 0 turns it off), default DH_MT_TB; used from DH_MT_MIN_TABLES tables (AUTO) on surfaces with
-// absolute strikes whose option threads are 128 or 256 per table.  Off by default: measured
-// (tools/gpu_r4_ab.sh) it loses on C3 / C4 with 256-thread tables (2 tables:
-// 60.7 -> 73 us, C4 235 -> 326 us: 512-thread blocks leave half a CU waiting in their serial
-// phases) and gains 3% on C3 only with 128-thread tables (59.2 us), which cost the one-table
-// kernel 6%.  DH_PATH_FUSED_MT still selects it (the same bits as every other path).
-#ifndef DH_MT_TB
-#define DH_MT_TB 0
-#endif
-#ifndef DH_MT_MIN_TABLES
-#define DH_MT_MIN_TABLES 2048
-#endif
-int mt_tables_per_block(dh_ctx* ctx) {
-    if (ctx->mt_tb < 0) {
-        int tb = DH_MT_TB;
-        if (const char* e = std::getenv("DHCOS_MT_TB")) tb = std::atoi(e);
-        ctx->mt_tb = (tb == 2 || tb == 4) ? tb : 0;
-    }
-    return ctx->mt_tb;
-}
-
-size_t mt_lds_bytes(int TB, int TT, int N, int cap) {
-    return ((size_t)mt_shared_doubles(cap) + (size_t)TB * mt_table_doubles(N, cap, TT)) *
-           sizeof(double);
-}
-
-// 0 if cos_fused_mt_kernel does not apply to the request, else its tables per block
-int mt_applies(dh_ctx* ctx, const PriceArgs& A0) {
-    const int TB = mt_tables_per_block(ctx);
-    if (!TB || A0.paired || A0.strike_mode != DH_STRIKE_ABSOLUTE || ctx->stamps_on) return 0;
-    const int TT = option_tpt(A0.opt_cap, A0.N, A0.opt_cap);
-    if (A0.max_group > kTileMax || (TT != kBlock && TT != kBlock / 2)) return 0;
-    if (mt_lds_bytes(TB, TT, A0.N, A0.opt_cap) > (size_t)kLdsDyn) return 0;
-    return TB;
-}
-
-int launch_fused_mt(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st, int TB) {
-    const int tpp = A0.n_groups;
-    const int64_t pb = (A0.P + TB - 1) / TB;
-    const int64_t blocks = pb * tpp;
-    if (blocks > 0x7fffffffLL) return fail(DH_E_ARG, "launch too large");
-    PriceArgs A = A0;
-    A.p0 = 0;
-    A.np = A0.P;
-    const int TT = option_tpt(A.opt_cap, A.N, A.opt_cap);
-    const size_t lds = mt_lds_bytes(TB, TT, A.N, A.opt_cap);
-    const bool r1 = tile_r(A.opt_cap, TT) == 1;
-    const dim3 grid((unsigned)blocks), block((unsigned)(TB * TT));
-    const double* tsrc = A.group_T;
-#define DH_MT_LAUNCH(tb, tt, rt) hipLaunchKernelGGL((cos_fused_mt_kernel<tb, tt, rt>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, tpp, (int)pb, A)
-    const int key = TB * 1000 + TT * (r1 ? 1 : -1);
-    switch (key) {
-        case 2256: DH_MT_LAUNCH(2, 256, 1); break;
-        case 2000 - 256: DH_MT_LAUNCH(2, 256, kR); break;
-        case 4256: DH_MT_LAUNCH(4, 256, 1); break;
-        case 4000 - 256: DH_MT_LAUNCH(4, 256, kR); break;
-        case 2128: DH_MT_LAUNCH(2, 128, 1); break;
-        case 2000 - 128: DH_MT_LAUNCH(2, 128, kR); break;
-        case 4128: DH_MT_LAUNCH(4, 128, 1); break;
-        case 4000 - 128: DH_MT_LAUNCH(4, 128, kR); break;
-        default: return fail(DH_E_ARG, "multi-table kernel shape");
-    }
-#undef DH_MT_LAUNCH
-    HIP_TRY(hipGetLastError());
-    return DH_OK;
-}
-
 // The generator batch path: every maturity group one tile of <= kSmallTile options, a large call
 // (DESIGN.md 3.3): one persistent cos_gen_kernel launch for the whole request.
 int launch_gen(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st, int TB) {
@@ -3022,19 +2586,9 @@ int launch_price(dh_ctx* ctx, const PriceArgs& A_in, hipStream_t st) {
         // whose lane-per-option-group kernel is 1.7x faster); measured on the current kernels:
         // C3 113 vs 133 us, C4 393 vs 407 us per request
         const bool fused = fusable && (ctx->path == DH_PATH_FUSED ||
-                                       ctx->path == DH_PATH_FUSED_MT ||
                                        (ctx->path == DH_PATH_AUTO && !small_call));
         ctx->last_path = fused ? DH_PATH_FUSED : DH_PATH_SPLIT;
-        if (fused) {
-            const int mt = mt_applies(ctx, A0);
-            const int64_t tables = A0.P * (A0.paired ? 1 : A0.n_groups);
-            if (mt && (ctx->path == DH_PATH_FUSED_MT ||
-                       (ctx->path == DH_PATH_AUTO && tables >= DH_MT_MIN_TABLES))) {
-                ctx->last_path = DH_PATH_FUSED_MT;
-                return launch_fused_mt(ctx, A0, st, mt);
-            }
-            return launch_fused(ctx, A0, st);
-        }
+        if (fused) return launch_fused(ctx, A0, st);
         // generator grids: one fused small-tile launch (PATH_SPLIT keeps the table + option
         // kernels, for A/B)
         const int tb = gen_tb(N);
@@ -3242,8 +2796,7 @@ int dh_ctx_read_stamps(dh_ctx* ctx, unsigned long long* out, int64_t cap, int64_
 
 int dh_ctx_set_path(dh_ctx* ctx, int path) {
     if (!ctx) return fail(DH_E_ARG, "ctx is null");
-    if (path != DH_PATH_AUTO && path != DH_PATH_SPLIT && path != DH_PATH_FUSED &&
-        path != DH_PATH_FUSED_MT)
+    if (path != DH_PATH_AUTO && path != DH_PATH_SPLIT && path != DH_PATH_FUSED)
         return fail(DH_E_ARG, "bad path");
     ctx->path = path;
     return DH_OK;
@@ -3517,15 +3070,26 @@ int dh_surface_price_cols(dh_ctx* ctx, const dh_surface* s, const double* params
     return DH_OK;
 }
 
+// A failed (un)registration is reported here and nowhere else: HIP's per-thread last error is
+// read back (cleared), so the next call's hipGetLastError check after a launch does not report it
+// (a caller that leaves an array pageable after a failed registration, _native.pinned, goes on)
 int dh_host_register(void* ptr, size_t bytes) {
     if (!ptr || !bytes) return fail(DH_E_ARG, "null or empty range");
-    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(DH_E_HIP, std::string("hipHostRegister: ") + hipGetErrorString(e));
+    }
     return DH_OK;
 }
 
 int dh_host_unregister(void* ptr) {
     if (!ptr) return fail(DH_E_ARG, "null argument");
-    HIP_TRY(hipHostUnregister(ptr));
+    const hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(DH_E_HIP, std::string("hipHostUnregister: ") + hipGetErrorString(e));
+    }
     return DH_OK;
 }
 
@@ -4300,8 +3864,7 @@ extern "C" int dh_calibrate_lbfgs(dh_ctx* ctx, const dh_surface* s, const double
                                         (int32_t*)A.bad, nullptr, st, A.live_count, true);
             if (e) return e;
             // a fused request stored its tile partials only (no hand-off): the step sums them
-            A.part_mode = !per_term(ctx, N) && (ctx->last_path == DH_PATH_FUSED ||
-                                                ctx->last_path == DH_PATH_FUSED_MT) ? 1 : 0;
+            A.part_mode = !per_term(ctx, N) && ctx->last_path == DH_PATH_FUSED ? 1 : 0;
             A.part_sse = (const double*)ctx->part_sse.ptr;
             e = launch_lb_step(st, A, n_live);
             if (e) return e;

@@ -27,7 +27,6 @@ MAX_N_PER_TERM = 65536         # longest accepted; longer than MAX_N runs the pe
 STRIKE_ABSOLUTE = 0
 STRIKE_PCT_SPOT = 1
 PATH_AUTO, PATH_SPLIT, PATH_FUSED, PATH_GEN = 0, 1, 2, 3   # PATH_GEN: reported only (AUTO)
-PATH_FUSED_MT = 4              # several tables per block (dh_ctx_set_path; AUTO on large grids)
 STAMPS_PER_BLOCK = 32          # kStamps of the DH_STAMPS build (csrc/dh_kernels.hip)
 
 _dp = C.POINTER(C.c_double)
@@ -209,8 +208,7 @@ class Context:
 
     def set_path(self, path: int):
         """Request kernels: PATH_AUTO (default), PATH_SPLIT (table + option launches),
-        PATH_FUSED (one launch per request where every maturity group is one tile) or
-        PATH_FUSED_MT (that launch with several tables per block, where it applies)."""
+        or PATH_FUSED (one launch per request where every maturity group is one tile)."""
         _check(load().dh_ctx_set_path(self._h, int(path)))
 
     @property
@@ -774,10 +772,12 @@ _tls = threading.local()
 def resolve_device(device: int | None = None) -> int:
     """The GPU a call without an explicit ``device=`` runs on, in this order: $DHCOS_DEVICE;
     under torch.distributed (one process per GPU, e.g. torchrun) the device the rank bound --
-    the process group's ``device_id``, else torch's current device when ``torch.cuda.set_device``
-    moved it off the default 0 -- then $LOCAL_RANK modulo the visible devices (a gloo job that
-    never binds a device: each rank its own GPU, not all on GPU 0); otherwise 0.
-    ``distributed._comm_device`` puts the collectives' tensors on the same GPU."""
+    the process group's ``device_id``, else torch's current device once the rank has set up its
+    CUDA state (``torch.cuda.set_device``, any CUDA tensor: whatever rank-to-GPU map the caller
+    used, device 0 included, so this library's GPU is its tensors' and collectives' GPU) -- then
+    $LOCAL_RANK modulo the visible devices (a gloo job that never touched CUDA: each rank its own
+    GPU, not all on GPU 0); otherwise 0.  ``distributed._comm_device`` puts the collectives'
+    tensors on the same GPU."""
     if device is not None:
         return int(device)
     env = os.environ.get("DHCOS_DEVICE")
@@ -793,9 +793,8 @@ def resolve_device(device: int | None = None) -> int:
                 bound = None
             if bound is not None and bound.type == "cuda" and bound.index is not None:
                 return int(bound.index)
-            cur = int(torch.cuda.current_device())
-            if cur != 0:
-                return cur
+            if torch.cuda.is_initialized():
+                return int(torch.cuda.current_device())
         local = os.environ.get("LOCAL_RANK")
         if local not in (None, ""):
             n = device_count()
@@ -843,7 +842,7 @@ def default_context(device: int | None = None) -> Context:
 __all__ = ["gen_draw", "gen_assemble", "gen_dates", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "MAX_N_PER_TERM",
            "STRIKE_ABSOLUTE",
-           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN", "PATH_FUSED_MT",
+           "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN",
            "LIB_PATH",
            "SIGNATURES",
            "Comm", "comm_id", "best_start", "COMM_ID_BYTES", "FgChannel", "pinned"]

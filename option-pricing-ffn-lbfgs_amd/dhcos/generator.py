@@ -151,8 +151,16 @@ def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES,
                                             strike_mode=_native.STRIKE_PCT_SPOT)
     n = params.shape[0]
     out = np.empty((n, T.size))
-    params, spots = np.ascontiguousarray(params, dtype=np.float64), np.ascontiguousarray(
-        spots, dtype=np.float64)
+    if ready is not None:
+        # rows are still being written (a draw in progress): a converting copy would snapshot
+        # rows the draw has not finished, so the arrays must be the draw's own
+        for a in (params, spots):
+            if a.dtype != np.float64 or not a.flags.c_contiguous:
+                raise ValueError("price_grid(ready=...): params / spots must be the draw's "
+                                 "C-contiguous float64 arrays")
+    else:
+        params = np.ascontiguousarray(params, dtype=np.float64)
+        spots = np.ascontiguousarray(spots, dtype=np.float64)
     # the rows move by DMA from / into the page-locked arrays; the device forms the records
     with _native.pinned(params, spots, out):
         for s in range(0, n, chunk):

@@ -201,25 +201,30 @@ def test_missing_outcome_record_never_wins():
 
 
 def test_resolve_device_under_process_group(monkeypatch):
-    """Under torch.distributed on a multi-GPU node: a gloo job that never binds a device puts
-    rank LOCAL_RANK on its own GPU (not every rank on torch's default GPU 0); a device moved with
-    torch.cuda.set_device wins over LOCAL_RANK.  (GPUs simulated: 8 visible.)"""
+    """Under torch.distributed on a multi-GPU node: a gloo job that never touched CUDA puts
+    rank LOCAL_RANK on its own GPU (not every rank on torch's default GPU 0); once the rank has
+    a CUDA state, torch's current device wins over LOCAL_RANK -- set_device(5), and also an
+    explicit set_device(0) with LOCAL_RANK = 3 (the caller's own rank-to-GPU map).  (GPUs
+    simulated: 8 visible.)"""
     import torch
     from dhcos import _native
     monkeypatch.delenv("DHCOS_DEVICE", raising=False)
     monkeypatch.setenv("LOCAL_RANK", "3")
     monkeypatch.setattr(_native, "device_count", lambda: 8)
     monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
-    cur = {"dev": 0}
+    cur = {"dev": 0, "init": False}
     monkeypatch.setattr(torch.cuda, "current_device", lambda: cur["dev"])
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: cur["init"])
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
-        assert _native.resolve_device() == 3          # unbound: LOCAL_RANK
-        cur["dev"] = 5
+        assert _native.resolve_device() == 3          # no CUDA state: LOCAL_RANK
+        cur.update(dev=5, init=True)
         assert _native.resolve_device() == 5          # set_device(5)
+        cur.update(dev=0, init=True)
+        assert _native.resolve_device() == 0          # set_device(0) under LOCAL_RANK = 3
         monkeypatch.setenv("LOCAL_RANK", "11")
-        cur["dev"] = 0
+        cur.update(dev=0, init=False)
         assert _native.resolve_device() == 3          # modulo the visible GPUs
     finally:
         dist.destroy_process_group()

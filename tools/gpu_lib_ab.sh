@@ -1,20 +1,13 @@
 #!/bin/bash
 # A/B of library variants on one box: LIBS="base g5 ..." CONFIG=c3 tools/gpu_lib_ab.sh
-# (base = libdhcos.so, mtK = libdhcos.so with $DHCOS_MT_TB=K, X = libdhcos_X.so, X:mtK both); two
-# alternations, ms_per_step and kernel_ms per run.
+# (base = libdhcos.so, X = libdhcos_X.so); two alternations, ms_per_step and kernel_ms per run.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out/ab
 CONFIG=${CONFIG:-c3}
 for rep in 1 2; do
   for v in ${LIBS:-base}; do
-    unset DHCOS_MT_TB DHCOS_LIB
-    lib=${v%%:*}; opt=""; [ "$lib" != "$v" ] && opt=${v#*:}      # LIB[:mtK]
-    case $lib in
-      base) ;;
-      mt*) opt=$lib ;;
-      *) export DHCOS_LIB=$PWD/option-pricing-ffn-lbfgs_amd/dhcos/libdhcos_$lib.so ;;
-    esac
-    case $opt in mt*) export DHCOS_MT_TB=${opt#mt} ;; esac       # mt0 / mt2 / mt4: tables per block
+    unset DHCOS_LIB
+    [ "$v" != base ] && export DHCOS_LIB=$PWD/option-pricing-ffn-lbfgs_amd/dhcos/libdhcos_$v.so
     timeout -k 10 120 python3 bench.py --config $CONFIG --path ${BPATH:-auto} --no-cpu --no-calib --no-side --steps ${STEPS:-200} --warmup 20 \
         > gpurun_out/ab/${CONFIG}_${v}_$rep.json 2> gpurun_out/ab/${CONFIG}_${v}_$rep.err || { echo "$v failed"; tail -3 gpurun_out/ab/${CONFIG}_${v}_$rep.err; exit 1; }
     python3 -c "

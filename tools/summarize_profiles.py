@@ -23,7 +23,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("cos_fused_mt_kernel", "cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel",
+KERNELS = ("cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel",
            "table_prologue_kernel", "cos_gen_kernel")
 
 
@@ -57,9 +57,7 @@ def main():
           "kernel (--path split; cos_option_kernel for multi-tile groups, "
           "cos_option_small_kernel for large calls on <=16-option tiles). Durations: "
           "rocprofv3 --kernel-trace --stats average; counters: per-launch medians of separate "
-          "--pmc passes.  (cos_fused_mt_kernel, several param sets of one maturity group per "
-          "block, runs only under dh_ctx_set_path(PATH_FUSED_MT) / $DHCOS_MT_TB: measured "
-          "slower in round 4.)", ""]
+          "--pmc passes.", ""]
     for c in args.configs.split(","):
         stats = os.path.join(args.src, f"{args.tag}_{c}_stats_kernel_stats.csv")
         if not os.path.exists(stats):
