@@ -249,6 +249,35 @@ int dh_gen_draw_progress(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,
                          const double* hi, int n_opt, double alpha, double spot0, double ret_mu,
                          double ret_sigma, double noise_sigma, double* params, double* spots,
                          double* noise, int64_t* done);
+/* ---- sharded draw (generate_sharded): one rank locates, every rank draws its own samples -- */
+/* The serial part of the draw only (the MT19937 twister, the polar method's acceptance bitmaps
+ * and the walk over them; no sample is drawn): for each of n_starts sample indices starts[]
+ * (non-decreasing, <= n_samples) the generator's state at that sample's first draw, as
+ * DH_GEN_LOC_WORDS doubles at loc[j * DH_GEN_LOC_WORDS]: key[624], pos, has_gauss, cached gauss
+ * (np.random.get_state()'s fields).  The state arguments are advanced in place to where
+ * dh_gen_draw of n_samples would leave them.  Replaces the stream positions the reference's
+ * per-sample loop reaches (synthetic_generator.py:98-141).                                      */
+#define DH_GEN_LOC_WORDS 627
+int dh_gen_locate(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* cached_gauss,
+                  int64_t n_samples, int n_opt, const int64_t* starts, int64_t n_starts,
+                  double* loc);
+/* Draw samples [starts[0], i_end) from located states: chunk j = [starts[j], starts[j + 1]) (the
+ * last ends at i_end) from loc[j], chunks in parallel on the host's threads.  Rows relative to
+ * starts[0]: params [n][13] the raw uniforms (:100-102, before the AR(1) blend), rets [n] the spot
+ * return's normal(0.0003, 0.01) draw (:112-116; sample 0 has none), noise [n][n_opt] (:141).   */
+int dh_gen_draw_located(const double* loc, const int64_t* starts, int64_t n_starts,
+                        int64_t i_end, const double* lo, const double* hi, int n_opt,
+                        double ret_mu, double ret_sigma, double noise_sigma, double* params,
+                        double* rets, double* noise);
+/* The values that carry across samples, over rows [0, n) = samples [i0, i0 + n): the AR(1) blend
+ * params[i] = alpha params[i - 1] + (1 - alpha) raw[i] (:105-109) and the spot walk spot[i] =
+ * spot[i - 1] (1 + ret[i]) (:112-116), in place (spots: rets in, spots out).  carry [14] holds
+ * the previous sample's blended params and spot (ignored when i0 = 0: spot0 starts the walk)
+ * and receives this block's last row: the 14 doubles one rank passes to the next.            */
+int dh_gen_sweep(double* params, double* spots, int64_t i0, int64_t n, double alpha, double spot0,
+                 double* carry);
+/* Samples drawn by this process's draw calls so far (instrumentation of the sharded draw).    */
+int dh_gen_drawn_samples(int64_t* count);
 /* The generator's trading dates (synthetic_generator.py:59-67: weekdays from a Monday, here
  * 2022-01-03 = day 18995 since 1970-01-01, as 'YYYY-MM-DD'): sample i's date as 10 UCS-4 code
  * points at out[10 i] (a NumPy '<U10' array's buffer).  DH_E_ARG past year 9999.             */

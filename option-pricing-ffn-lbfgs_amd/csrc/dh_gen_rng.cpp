@@ -273,6 +273,9 @@ double now_s() {
 constexpr int64_t kChunk = 1 << 16;
 constexpr int64_t kSplitMin = 4096;
 
+// samples drawn (uniforms, gauss calls, noise) by this process's draw calls (dh_gen_drawn_samples)
+std::atomic<int64_t> g_drawn_total{0};
+
 }  // namespace
 
 namespace {
@@ -363,6 +366,8 @@ struct ParDraw {
     int pos0 = 0;
     uint32_t key0[kMtN];
     int64_t n = 0, n_opt = 0, n_chunks = 0, max_t = 0, max_blocks = 0;
+    // chunk c covers samples [starts[c], starts[c + 1]) (starts[n_chunks] = n)
+    std::vector<int64_t> starts;
     // published by the twister: keys of generations 64 b
     std::vector<uint32_t> snaps;
     std::atomic<int64_t> snaps_ready{0};
@@ -371,9 +376,11 @@ struct ParDraw {
     std::vector<std::atomic<uint8_t>> block_done;
     std::atomic<int64_t> next_block{0};
     std::atomic<int64_t> walker_block{0};
-    // the walk's chunk starts
+    // the walk's chunk starts: double index, has_gauss, and the last accepted pair before it
+    // (its first double's index; -1: none since the entry)
     std::vector<int64_t> chunk_t;
     std::vector<int32_t> chunk_hg;
+    std::vector<int64_t> chunk_lp;
     std::atomic<int64_t> chunks_located{0};
     std::atomic<int64_t> next_chunk{0};
     std::vector<std::atomic<uint8_t>> chunk_done;
@@ -383,7 +390,7 @@ struct ParDraw {
     std::vector<int64_t> chunk_fb_i;
     std::vector<int32_t> chunk_fb_j;
     std::atomic<bool> walk_done{false}, failed{false};
-    int64_t t_end = 0;
+    int64_t t_end = 0, lp_end = -1;
     int hg_end = 0;
 
     // the first double of the block's range, and the block of double t
@@ -400,6 +407,39 @@ struct ParDraw {
         std::memcpy(r.key, k, sizeof(r.key));
         for (int64_t i = 0; i < g % kGensPerBlock; ++i) mt_twist(r.key);
         std::memcpy(k, r.key, sizeof(r.key));
+    }
+    // gen_key for any generation once the team has stopped: a block the twister never reached
+    // (a walk that needed no acceptance bits there) is twisted forward from the last published
+    // key, or from the entry key
+    void key_any(int64_t g, uint32_t* k) const {
+        const int64_t ready = snaps_ready.load(std::memory_order_acquire);
+        if (g / kGensPerBlock < ready) {
+            gen_key(g, k);
+            return;
+        }
+        const int64_t g0 = ready > 0 ? (ready - 1) * kGensPerBlock : 0;
+        std::memcpy(k, ready > 0 ? snaps.data() + (ready - 1) * kMtN : key0,
+                    sizeof(uint32_t) * kMtN);
+        for (int64_t i = g0; i < g; ++i) mt_twist(k);
+    }
+    // the generator positioned at double t of the stream (word pos0 + 2 t)
+    void rng_at(int64_t t, LegacyRng& r) const {
+        const int64_t w = pos0 + 2 * t;
+        key_any(w / kMtN, r.key);
+        r.pos = (int)(w % kMtN);
+        r.has_gauss = 0;
+        r.gauss = 0.0;
+    }
+    // the value next_gauss caches from the accepted pair at double t: f x1 (pair_values)
+    double pair_cached(int64_t t) const {
+        LegacyRng r;
+        rng_at(t, r);
+        const double x1 = 2.0 * r.next_double() - 1.0;
+        const double x2 = 2.0 * r.next_double() - 1.0;
+        const double r2 = x1 * x1 + x2 * x2;
+        double gn, gc;
+        pair_values(x1, x2, r2, gn, gc);
+        return gc;
     }
 };
 
@@ -529,16 +569,18 @@ int64_t par_select(ParDraw& P, int64_t t, int k, int64_t& ready_t, int64_t& next
     }
 }
 
-void par_walk(ParDraw& P, int hg0, int64_t chunk) {
+void par_walk(ParDraw& P, int hg0) {
     int64_t t = 0, ready_t = 0, next_b = 0, last_pair = -1;
     int hg = hg0;
     bool ok = true;
+    int64_t c = 0;
     for (int64_t i = 0; i < P.n && ok; ++i) {
-        if (i % chunk == 0) {
-            const int64_t c = i / chunk;
+        while (c < P.n_chunks && P.starts[c] == i) {     // (equal starts: empty chunks)
             P.chunk_t[c] = t;
             P.chunk_hg[c] = hg;
+            P.chunk_lp[c] = last_pair;
             P.chunks_located.store(c + 1, std::memory_order_release);
+            ++c;
         }
         t += 13;                                              // :100-102
         const int calls = (int)P.n_opt + (i > 0 ? 1 : 0);     // :112-116, :141
@@ -553,7 +595,14 @@ void par_walk(ParDraw& P, int hg0, int64_t chunk) {
     if (!ok || t >= P.max_t) {
         P.failed.store(true);
     }
+    for (; c < P.n_chunks; ++c) {                          // chunks starting at n (empty)
+        P.chunk_t[c] = t;
+        P.chunk_hg[c] = hg;
+        P.chunk_lp[c] = last_pair;
+    }
+    P.chunks_located.store(P.n_chunks, std::memory_order_release);
     P.t_end = t;
+    P.lp_end = last_pair;
     P.hg_end = hg;
     P.walk_done.store(true, std::memory_order_release);
 }
@@ -565,10 +614,11 @@ struct ChunkOut {
 // one chunk of the draw from its located start: raw uniforms into params (the blend is the
 // sweep's), noise, and the spot return's normal (ret_mu + ret_sigma g) into spots; a first gauss
 // call served from the value cached before the chunk is left to the sweep
-void par_chunk(ParDraw& P, int64_t c, int64_t chunk, const double* lo, const double* range,
+void par_chunk(ParDraw& P, int64_t c, const double* lo, const double* range,
                double ret_mu, double ret_sigma, double noise_sigma, double* params,
                double* spots, double* noise, ChunkOut& o) {
-    const int64_t c0 = c * chunk, c1 = std::min(P.n, c0 + chunk);
+    const int64_t c0 = P.starts[c], c1 = P.starts[c + 1];
+    g_drawn_total.fetch_add(c1 - c0, std::memory_order_relaxed);
     const int64_t word = P.pos0 + 2 * P.chunk_t[c];
     LegacyRng g;
     // the block's key may not be published yet (chunk 0 is located before the twister's first
@@ -637,22 +687,18 @@ void par_chunk(ParDraw& P, int64_t c, int64_t chunk, const double* lo, const dou
     P.chunk_done[c].store(1, std::memory_order_release);
 }
 
-// -> 1 done, 0 not applicable / bound exceeded (the caller runs the sequential draw instead)
-int gen_draw_parallel(LegacyRng& g, int64_t n_samples, const double* lo, const double* hi,
-                      int n_opt, double alpha, double spot0, double ret_mu, double ret_sigma,
-                      double noise_sigma, double* params, double* spots, double* noise,
-                      const std::function<void(int64_t)>& publish) {
-    const int nth = team_size();
-    if (nth < 3) return 0;
-    ParDraw P;
+// The stream geometry and buffers of a parallel pass over n_samples from g's state, with chunk
+// starts `starts` (sorted; starts[0] = 0, the last entry n_samples)
+void par_setup(ParDraw& P, const LegacyRng& g, int64_t n_samples, int n_opt,
+               std::vector<int64_t> starts) {
     LegacyRng e = g;
     if (e.pos == kMtN) e.twist();
     P.pos0 = e.pos;
     std::memcpy(P.key0, e.key, sizeof(P.key0));
     P.n = n_samples;
     P.n_opt = n_opt;
-    const int64_t chunk = kParChunk;
-    P.n_chunks = (n_samples + chunk - 1) / chunk;
+    P.starts = std::move(starts);
+    P.n_chunks = (int64_t)P.starts.size() - 1;
     // stream bound: twice the expected doubles (acceptance pi/4) plus slack; a walk past it
     // (never seen: ~thousands of standard deviations) falls back to the sequential draw
     const double per_sample = 13.0 + 2.0 * ((n_opt + 2) / 2) / 0.7853981633974483;
@@ -669,15 +715,80 @@ int gen_draw_parallel(LegacyRng& g, int64_t n_samples, const double* lo, const d
         std::vector<std::atomic<uint8_t>> v(P.max_blocks);
         P.block_done.swap(v);
         for (auto& a : P.block_done) a.store(0, std::memory_order_relaxed);
-        std::vector<std::atomic<uint8_t>> u(P.n_chunks);
+        std::vector<std::atomic<uint8_t>> u(std::max<int64_t>(P.n_chunks, 0));
         P.chunk_done.swap(u);
         for (auto& a : P.chunk_done) a.store(0, std::memory_order_relaxed);
     }
-    P.chunk_t.assign(P.n_chunks, 0);
-    P.chunk_hg.assign(P.n_chunks, 0);
-    P.chunk_last_gc.assign(P.n_chunks, NAN);
-    P.chunk_fb_i.assign(P.n_chunks, -1);
-    P.chunk_fb_j.assign(P.n_chunks, -1);
+    const int64_t nc = std::max<int64_t>(P.n_chunks, 0);
+    P.chunk_t.assign(nc, 0);
+    P.chunk_hg.assign(nc, 0);
+    P.chunk_lp.assign(nc, -1);
+    P.chunk_last_gc.assign(nc, NAN);
+    P.chunk_fb_i.assign(nc, -1);
+    P.chunk_fb_j.assign(nc, -1);
+}
+
+// A bit worker (and, with draw, a chunk worker) of the team until the pass is over
+void par_worker(ParDraw& P, bool draw, const double* lo, const double* range, double ret_mu,
+                double ret_sigma, double noise_sigma, double* params, double* spots,
+                double* noise) {
+    BitsScratch wbuf;
+    ChunkOut out;
+    for (;;) {
+        if (P.failed.load()) return;
+        const bool walking = !P.walk_done.load(std::memory_order_acquire);
+        const int64_t b = P.next_block.load(std::memory_order_relaxed);
+        if (walking && b < P.snaps_ready.load(std::memory_order_acquire) &&
+            b <= P.walker_block.load(std::memory_order_relaxed) + kLookahead) {
+            int64_t bb = b;
+            if (P.next_block.compare_exchange_weak(bb, b + 1)) par_bits(P, b, wbuf);
+            continue;
+        }
+        if (draw) {
+            const int64_t c = P.next_chunk.load(std::memory_order_relaxed);
+            if (c < P.chunks_located.load(std::memory_order_acquire)) {
+                int64_t cc = c;
+                if (P.next_chunk.compare_exchange_weak(cc, c + 1))
+                    par_chunk(P, c, lo, range, ret_mu, ret_sigma, noise_sigma, params, spots,
+                              noise, out);
+                continue;
+            }
+            if (!walking && c >= P.n_chunks) return;
+        } else if (!walking) {
+            return;
+        }
+        spin_pause();
+    }
+}
+
+// The state the sequential loop leaves after the pass (its walk's end): word n_end = 2 t_end of
+// the stream read, has_gauss and the value cached from the last pair (or kept from the entry)
+void par_final_state(const ParDraw& P, const LegacyRng& entry, LegacyRng& g) {
+    const int64_t n_end = 2 * P.t_end;
+    const double entry_gauss = entry.gauss;
+    if (n_end > 0) {
+        const int64_t last = P.pos0 + n_end - 1;             // the last word read
+        P.key_any(last / kMtN, g.key);
+        g.pos = (int)(last % kMtN) + 1;                      // 1 .. 624 (624: twist pending)
+    } else {
+        g = entry;                                           // nothing read: the entry state
+    }
+    g.has_gauss = P.hg_end;
+    g.gauss = P.hg_end ? (P.lp_end >= 0 ? P.pair_cached(P.lp_end) : entry_gauss) : 0.0;
+}
+
+// -> 1 done, 0 not applicable / bound exceeded (the caller runs the sequential draw instead)
+int gen_draw_parallel(LegacyRng& g, int64_t n_samples, const double* lo, const double* hi,
+                      int n_opt, double alpha, double spot0, double ret_mu, double ret_sigma,
+                      double noise_sigma, double* params, double* spots, double* noise,
+                      const std::function<void(int64_t)>& publish) {
+    const int nth = team_size();
+    if (nth < 3) return 0;
+    ParDraw P;
+    std::vector<int64_t> starts;
+    for (int64_t i = 0; i < n_samples; i += kParChunk) starts.push_back(i);
+    starts.push_back(n_samples);
+    par_setup(P, g, n_samples, n_opt, std::move(starts));
     double range[13];
     for (int j = 0; j < 13; ++j) range[j] = hi[j] - lo[j];
     const double beta = 1.0 - alpha;
@@ -694,7 +805,7 @@ int gen_draw_parallel(LegacyRng& g, int64_t n_samples, const double* lo, const d
             w = 2;                            // then a worker like the others
         }
         if (w == 0) {
-            par_walk(P, g.has_gauss ? 1 : 0, chunk);
+            par_walk(P, g.has_gauss ? 1 : 0);
             t_walk = now_s() - t_start;
             if (P.failed.load()) {
                 fell_back = true;
@@ -706,7 +817,7 @@ int gen_draw_parallel(LegacyRng& g, int64_t n_samples, const double* lo, const d
                     if (P.failed.load()) return;
                     spin_pause();
                 }
-                const int64_t c0 = c * chunk, c1 = std::min(n_samples, c0 + chunk);
+                const int64_t c0 = P.starts[c], c1 = P.starts[c + 1];
                 const int64_t fi = P.chunk_fb_i[c];   // served from before the chunk
                 if (fi >= 0) {
                     if (P.chunk_fb_j[c] < 0) spots[fi] = ret_mu + ret_sigma * pending;
@@ -728,29 +839,7 @@ int gen_draw_parallel(LegacyRng& g, int64_t n_samples, const double* lo, const d
             }
             return;
         }
-        BitsScratch wbuf;
-        ChunkOut out;
-        for (;;) {
-            if (P.failed.load()) return;
-            const bool walking = !P.walk_done.load(std::memory_order_acquire);
-            const int64_t b = P.next_block.load(std::memory_order_relaxed);
-            if (walking && b < P.snaps_ready.load(std::memory_order_acquire) &&
-                b <= P.walker_block.load(std::memory_order_relaxed) + kLookahead) {
-                int64_t bb = b;
-                if (P.next_block.compare_exchange_weak(bb, b + 1)) par_bits(P, b, wbuf);
-                continue;
-            }
-            const int64_t c = P.next_chunk.load(std::memory_order_relaxed);
-            if (c < P.chunks_located.load(std::memory_order_acquire)) {
-                int64_t cc = c;
-                if (P.next_chunk.compare_exchange_weak(cc, c + 1))
-                    par_chunk(P, c, chunk, lo, range, ret_mu, ret_sigma, noise_sigma, params,
-                              spots, noise, out);
-                continue;
-            }
-            if (!walking && c >= P.n_chunks) return;
-            spin_pause();
-        }
+        par_worker(P, true, lo, range, ret_mu, ret_sigma, noise_sigma, params, spots, noise);
     });
     if (std::getenv("DHCOS_GEN_TIMING"))
         std::fprintf(stderr, "dh_gen_draw (parallel, %d threads): %lld samples: twister %.4f s, "
@@ -758,22 +847,141 @@ int gen_draw_parallel(LegacyRng& g, int64_t n_samples, const double* lo, const d
                      t_twist, t_walk, now_s() - t_start,
                      (long long)P.snaps_ready.load());
     if (fell_back || P.failed.load()) return 0;
-    // the state the sequential loop leaves: word n_end = 2 t_end of the stream read
-    const int64_t n_end = 2 * P.t_end;
-    if (n_end > 0) {
-        const int64_t last = P.pos0 + n_end - 1;             // the last word read
-        const int64_t gl = last / kMtN;
-        uint32_t k[kMtN];
-        if (gl == 0) std::memcpy(k, P.key0, sizeof(k));
-        else P.gen_key(gl, k);
-        std::memcpy(g.key, k, sizeof(k));
-        g.pos = (int)(last % kMtN) + 1;                      // 1 .. 624 (624: twist pending)
-    } else {
-        g = e;
-    }
-    g.has_gauss = P.hg_end;
-    g.gauss = P.hg_end ? pending : 0.0;
+    const LegacyRng entry = g;
+    par_final_state(P, entry, g);
+    g.gauss = g.has_gauss ? pending : 0.0;    // (par_final_state's value, via the sweep)
     return 1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sharded draw (round 5): one rank locates, every rank draws its own samples.
+//   locate:  the serial part of the parallel draw only -- the twister, the acceptance bitmaps
+//            and the walk -- recording the generator's state (key, pos, has_gauss, cached value:
+//            np.random.get_state()'s fields) at the first sample of each requested chunk;
+//   located: a rank draws its chunks from those states (uniforms, accepted pairs, log / sqrt,
+//            noise and the spot return's normal; no AR(1), no spot walk);
+//   sweep:   the values that carry across samples (the AR(1) blend and the spot walk) over a
+//            rank's block, from the previous block's last row (14 doubles passed rank to rank).
+// The same words through the same operations in the same order as the sequential loop.
+// ---------------------------------------------------------------------------------------------
+constexpr int kLocWords = kMtN + 3;           // key[624], pos, has_gauss, cached (as doubles)
+
+void loc_store(const LegacyRng& r, double* out) {
+    for (int i = 0; i < kMtN; ++i) out[i] = (double)r.key[i];
+    out[kMtN] = r.pos;
+    out[kMtN + 1] = r.has_gauss;
+    out[kMtN + 2] = r.gauss;
+}
+
+bool loc_load(const double* in, LegacyRng& r) {
+    for (int i = 0; i < kMtN; ++i) {
+        const double v = in[i];
+        if (!(v >= 0.0 && v <= 4294967295.0) || v != (double)(uint32_t)v) return false;
+        r.key[i] = (uint32_t)v;
+    }
+    if (!(in[kMtN] >= 0.0 && in[kMtN] <= kMtN) || in[kMtN] != (int)in[kMtN]) return false;
+    r.pos = (int)in[kMtN];
+    r.has_gauss = in[kMtN + 1] != 0.0 ? 1 : 0;
+    r.gauss = in[kMtN + 2];
+    return true;
+}
+
+// samples [i0, i1) from r's state (positioned at sample i0's first double): raw uniforms into
+// params, the spot return's normal (ret_mu + ret_sigma g) into rets for i > 0, noise; rows
+// relative to `base`
+void draw_raw(LegacyRng r, int64_t i0, int64_t i1, int64_t base, const double* lo,
+              const double* range, int n_opt, double ret_mu, double ret_sigma, double noise_sigma,
+              double* params, double* rets, double* noise) {
+    g_drawn_total.fetch_add(i1 - i0, std::memory_order_relaxed);
+    const int kmax = (n_opt + 2) / 2;
+    std::vector<double> x1(kmax), x2(kmax), r2(kmax), gn(kmax), gc(kmax);
+    int hg = r.has_gauss;
+    double cached = r.gauss;
+    DoubleStream ds(r);
+    for (int64_t i = i0; i < i1; ++i) {
+        double* p = params + (i - base) * 13;
+        for (int j = 0; j < 13; ++j) p[j] = lo[j] + range[j] * ds.next();   // :100-102
+        const int calls = n_opt + (i > 0 ? 1 : 0);                           // :112-116, :141
+        const int fresh = calls - hg;
+        const int k = fresh > 0 ? (fresh + 1) / 2 : 0;
+        ds.pairs(k, x1.data(), x2.data(), r2.data());
+        for (int q = 0; q < k; ++q) pair_values(x1[q], x2[q], r2[q], gn[q], gc[q]);
+        // gauss call c of this sample: the value cached before it first, then the new pairs,
+        // each serving f x2 then f x1
+        auto value = [&](int c) {
+            if (hg) {
+                if (c == 0) return cached;
+                --c;
+            }
+            return (c & 1) ? gc[c / 2] : gn[c / 2];
+        };
+        const int c00 = i > 0 ? 1 : 0;
+        if (i > 0) rets[i - base] = ret_mu + ret_sigma * value(0);
+        double* z = noise + (i - base) * n_opt;
+        for (int j = 0; j < n_opt; ++j) z[j] = 0.0 + noise_sigma * value(c00 + j);
+        if (fresh > 0) {
+            hg = fresh & 1;
+            if (hg) cached = gc[k - 1];
+        } else {
+            hg -= calls;
+        }
+    }
+}
+
+}  // namespace
+
+namespace {
+
+int gen_locate(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* cached_gauss,
+               int64_t n_samples, int n_opt, const int64_t* starts, int64_t n_starts,
+               double* loc) {
+    if (!mt_key || !mt_pos || !has_gauss || !cached_gauss) return DH_E_ARG;
+    if (n_samples < 0 || n_opt < 0 || n_starts < 0 || (n_starts > 0 && (!starts || !loc)))
+        return DH_E_ARG;
+    if (*mt_pos < 0 || *mt_pos > kMtN) return DH_E_ARG;
+    for (int64_t j = 0; j < n_starts; ++j)
+        if (starts[j] < 0 || starts[j] > n_samples || (j > 0 && starts[j] < starts[j - 1]))
+            return DH_E_ARG;
+    LegacyRng g;
+    std::memcpy(g.key, mt_key, sizeof(g.key));
+    g.pos = *mt_pos;
+    g.has_gauss = *has_gauss ? 1 : 0;
+    g.gauss = *cached_gauss;
+    const LegacyRng entry = g;
+    ParDraw P;
+    std::vector<int64_t> st(starts, starts + n_starts);
+    st.push_back(n_samples);
+    par_setup(P, g, n_samples, n_opt, std::move(st));
+    const int nth = std::max(3, team_size());
+    {
+        Team team(nth);
+        team.run([&](int w) {
+            if (w == 1) {
+                par_twister(P);
+                w = 2;
+            }
+            if (w == 0) {
+                par_walk(P, g.has_gauss ? 1 : 0);
+                return;
+            }
+            par_worker(P, false, nullptr, nullptr, 0.0, 0.0, 0.0, nullptr, nullptr, nullptr);
+        });
+    }
+    if (P.failed.load()) return DH_E_ARG;      // past the stream bound (never seen)
+    for (int64_t j = 0; j < n_starts; ++j) {
+        LegacyRng r;
+        P.rng_at(P.chunk_t[j], r);
+        r.has_gauss = P.chunk_hg[j];
+        r.gauss = r.has_gauss ? (P.chunk_lp[j] >= 0 ? P.pair_cached(P.chunk_lp[j]) : entry.gauss)
+                              : 0.0;
+        loc_store(r, loc + j * kLocWords);
+    }
+    par_final_state(P, entry, g);
+    std::memcpy(mt_key, g.key, sizeof(g.key));
+    *mt_pos = g.pos;
+    *has_gauss = g.has_gauss;
+    *cached_gauss = g.gauss;
+    return DH_OK;
 }
 
 }  // namespace
@@ -812,6 +1020,7 @@ int gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* cach
         publish(n_samples);
         return DH_OK;
     }
+    g_drawn_total.fetch_add(n_samples, std::memory_order_relaxed);   // (sequential paths)
     if (n_samples < kSplitMin) {
         for (int64_t i = 0; i < n_samples; ++i) {
             double* p = params + i * 13;
@@ -973,6 +1182,74 @@ extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss
                            double* spots, double* noise) {
     return gen_draw(mt_key, mt_pos, has_gauss, cached_gauss, n_samples, lo, hi, n_opt, alpha,
                     spot0, ret_mu, ret_sigma, noise_sigma, params, spots, noise, nullptr);
+}
+
+extern "C" int dh_gen_locate(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,
+                             double* cached_gauss, int64_t n_samples, int n_opt,
+                             const int64_t* starts, int64_t n_starts, double* loc) {
+    return gen_locate(mt_key, mt_pos, has_gauss, cached_gauss, n_samples, n_opt, starts, n_starts,
+                      loc);
+}
+
+extern "C" int dh_gen_draw_located(const double* loc, const int64_t* starts, int64_t n_starts,
+                                   int64_t i_end, const double* lo, const double* hi, int n_opt,
+                                   double ret_mu, double ret_sigma, double noise_sigma,
+                                   double* params, double* rets, double* noise) {
+    if (n_starts < 0 || n_opt < 0 || (n_starts > 0 && (!loc || !starts || !lo || !hi)))
+        return DH_E_ARG;
+    if (n_starts == 0) return DH_OK;
+    for (int64_t j = 0; j < n_starts; ++j)
+        if (starts[j] < 0 || (j > 0 && starts[j] < starts[j - 1])) return DH_E_ARG;
+    if (i_end < starts[n_starts - 1]) return DH_E_ARG;
+    const int64_t base = starts[0], n = i_end - base;
+    if (n > 0 && (!params || !rets || (n_opt > 0 && !noise))) return DH_E_ARG;
+    std::vector<LegacyRng> rs(n_starts);
+    for (int64_t j = 0; j < n_starts; ++j)
+        if (!loc_load(loc + j * kLocWords, rs[j])) return DH_E_ARG;
+    double range[13];
+    for (int j = 0; j < 13; ++j) range[j] = hi[j] - lo[j];
+    auto chunk = [&](int64_t j) {
+        const int64_t c1 = j + 1 < n_starts ? starts[j + 1] : i_end;
+        draw_raw(rs[j], starts[j], c1, base, lo, range, n_opt, ret_mu, ret_sigma, noise_sigma,
+                 params, rets, noise);
+    };
+    if (n_starts == 1 || n < kSplitMin) {
+        for (int64_t j = 0; j < n_starts; ++j) chunk(j);
+        return DH_OK;
+    }
+    std::atomic<int64_t> next{0};
+    Team team((int)std::min<int64_t>(team_size(), n_starts));
+    team.run([&](int) {
+        for (int64_t j; (j = next.fetch_add(1)) < n_starts;) chunk(j);
+    });
+    return DH_OK;
+}
+
+extern "C" int dh_gen_sweep(double* params, double* spots, int64_t i0, int64_t n, double alpha,
+                            double spot0, double* carry) {
+    if (i0 < 0 || n < 0 || !carry || (n > 0 && (!params || !spots))) return DH_E_ARG;
+    const double beta = 1.0 - alpha;                       // (1 - alpha), :108
+    double prev_spot = i0 > 0 ? carry[13] : spot0;
+    for (int64_t r = 0; r < n; ++r) {
+        double* p = params + r * 13;
+        if (i0 + r > 0) {
+            const double* q = r > 0 ? p - 13 : carry;
+            for (int j = 0; j < 13; ++j) p[j] = alpha * q[j] + beta * p[j];   // :105-109
+            prev_spot = prev_spot * (1.0 + spots[r]);                         // :112-116
+        }
+        spots[r] = prev_spot;
+    }
+    if (n > 0) {
+        for (int j = 0; j < 13; ++j) carry[j] = params[(n - 1) * 13 + j];
+        carry[13] = prev_spot;
+    }
+    return DH_OK;
+}
+
+extern "C" int dh_gen_drawn_samples(int64_t* count) {
+    if (!count) return DH_E_ARG;
+    *count = g_drawn_total.load(std::memory_order_relaxed);
+    return DH_OK;
 }
 
 extern "C" int dh_gen_draw_progress(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,

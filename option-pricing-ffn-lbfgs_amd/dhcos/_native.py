@@ -90,6 +90,12 @@ SIGNATURES = {
                                        _dp, C.c_int, C.c_double, C.c_double, C.c_double,
                                        C.c_double, C.c_double, _dp, _dp, _dp,
                                        C.POINTER(C.c_int64)]),
+    "dh_gen_locate": (C.c_int, [C.POINTER(C.c_uint32), _i32p, _i32p, _dp, C.c_int64, C.c_int,
+                                _vp, C.c_int64, _dp]),
+    "dh_gen_draw_located": (C.c_int, [_dp, _vp, C.c_int64, C.c_int64, _dp, _dp, C.c_int,
+                                      C.c_double, C.c_double, C.c_double, _dp, _dp, _dp]),
+    "dh_gen_sweep": (C.c_int, [_dp, _dp, C.c_int64, C.c_int64, C.c_double, C.c_double, _dp]),
+    "dh_gen_drawn_samples": (C.c_int, [C.POINTER(C.c_int64)]),
     "dh_gen_assemble": (C.c_int, [_dp, _dp, _dp, _dp, C.c_int64, C.c_int, _dp, _dp, _dp]),
     "dh_gen_dates": (C.c_int, [C.c_int64, C.c_int64, _vp]),
     "dh_price_batch": (C.c_int, [_vp, _dp, C.c_int64, _dp, _dp, _i8p, C.c_int, C.c_int,
@@ -733,6 +739,68 @@ class GenDraw:
         return self.params, self.spots, self.noise
 
 
+GEN_LOC_WORDS = 627            # DH_GEN_LOC_WORDS: key[624], pos, has_gauss, cached gauss
+
+
+def gen_locate(state, n_samples, n_opt, starts):
+    """dh_gen_locate: from an np.random legacy state (``[627]`` float64: key, pos, has_gauss,
+    cached gauss) the generator's state at each sample index of ``starts`` of an
+    ``n_samples``-sample draw, without drawing the samples -> (loc [len(starts), 627], the state
+    the whole draw leaves [627])."""
+    st = np.asarray(state, dtype=np.float64).reshape(GEN_LOC_WORDS)
+    key = st[:624].astype(np.uint32)
+    c_pos, c_has = C.c_int32(int(st[624])), C.c_int32(int(st[625]))
+    c_cached = C.c_double(float(st[626]))
+    starts = np.ascontiguousarray(starts, dtype=np.int64).reshape(-1)
+    loc = np.empty((starts.size, GEN_LOC_WORDS))
+    _check(load().dh_gen_locate(key.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(c_pos),
+                                C.byref(c_has), C.byref(c_cached), int(n_samples), int(n_opt),
+                                starts.ctypes.data if starts.size else None, starts.size,
+                                _ptr(loc)))
+    end = np.concatenate([key.astype(np.float64), [c_pos.value, c_has.value, c_cached.value]])
+    return loc, end
+
+
+def gen_draw_located(loc, starts, i_end, lo, hi, n_opt, ret_mu, ret_sigma, noise_sigma):
+    """dh_gen_draw_located: samples [starts[0], i_end) drawn from located states (chunk j from
+    loc[j]) -> (raw params [n, 13], spot returns [n] (row of sample 0 unset), noise [n, n_opt])."""
+    loc = _f64(loc).reshape(-1, GEN_LOC_WORDS)
+    starts = np.ascontiguousarray(starts, dtype=np.int64).reshape(-1)
+    if loc.shape[0] != starts.size:
+        raise NativeError("gen_draw_located: one state per chunk start")
+    n = int(i_end) - int(starts[0]) if starts.size else 0
+    if n < 0:
+        raise NativeError("gen_draw_located: i_end before the first start")
+    params, rets, noise = np.empty((n, 13)), np.empty(n), np.empty((n, int(n_opt)))
+    if starts.size:
+        _check(load().dh_gen_draw_located(_ptr(loc), starts.ctypes.data, starts.size, int(i_end),
+                                          _ptr(_f64(lo)), _ptr(_f64(hi)), int(n_opt),
+                                          float(ret_mu), float(ret_sigma), float(noise_sigma),
+                                          _ptr(params), _ptr(rets), _ptr(noise)))
+    return params, rets, noise
+
+
+def gen_sweep(params, spots, i0, alpha, spot0, carry):
+    """dh_gen_sweep in place on a block of samples [i0, i0 + n): AR(1) blend of the raw params
+    and the spot walk from the returns; carry [14] (the previous sample's params and spot) in,
+    this block's last row out (returned)."""
+    n = params.shape[0]
+    for a, shp in ((params, (n, 13)), (spots, (n,))):
+        if a.dtype != np.float64 or a.shape != shp or not a.flags.c_contiguous:
+            raise NativeError("gen_sweep: params [n, 13] and spots [n] must be C-contiguous float64")
+    carry = np.array(carry, dtype=np.float64).reshape(14)
+    _check(load().dh_gen_sweep(_ptr(params), _ptr(spots), int(i0), n, float(alpha), float(spot0),
+                               _ptr(carry)))
+    return carry
+
+
+def gen_drawn_samples() -> int:
+    """dh_gen_drawn_samples: samples this process's draw calls have drawn so far."""
+    c = C.c_int64(0)
+    _check(load().dh_gen_drawn_samples(C.byref(c)))
+    return c.value
+
+
 def gen_assemble(model, noise, spots, k_rel, out=None):
     """dh_gen_assemble: the generator's market prices, per-sample losses (np.mean's bits) and
     absolute strikes from [n, m] model prices and noise.  -> (market, loss, strikes), written into
@@ -839,7 +907,8 @@ def default_context(device: int | None = None) -> Context:
     return ctx
 
 
-__all__ = ["gen_draw", "gen_assemble", "gen_dates", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
+__all__ = ["gen_draw", "gen_assemble", "gen_dates", "gen_locate", "gen_draw_located", "gen_sweep",
+           "gen_drawn_samples", "GEN_LOC_WORDS", "LbOptions", "LbResult", "Context", "Surface", "NativeError", "load", "default_context", "device_count",
            "runtime_shared_with_torch", "resolve_device", "PARAM_STRIDE", "MAX_N", "MAX_N_PER_TERM",
            "STRIKE_ABSOLUTE",
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN",

@@ -12,11 +12,15 @@ is exchanged: the shards are independent and each rank drives its own GPU.
     RNG state after the draws, so the result, ``n_calls`` / ``best_loss`` (those of the last
     start) and every rank's ``np.random`` stream afterwards equal the single-process
     ``calibrate`` with the same RNG state.
-  * ``generate_sharded``: rank 0's ``np.random`` state is broadcast and every rank draws every
-    sample's random numbers in reference order (synthetic_generator.py:98-141) with the parallel
-    native draw; rank r prices a contiguous block of samples; one all-gather assembles the prices
-    on every rank; rank 0 builds and saves the reference output.  Every rank's ``np.random`` ends
-    where rank 0's draws left it.
+  * ``generate_sharded``: rank r owns a contiguous block of samples and draws only those.  Rank 0
+    runs the serial part of the draw alone -- the MT19937 twister, the polar acceptance bitmaps
+    and the walk (dh_gen_locate), no sample drawn -- and broadcasts the generator's state at the
+    start of every rank's chunks (627 words each).  Each rank draws its own chunks
+    (dh_gen_draw_located), the AR(1) blend and spot walk pass rank to rank (the previous block's
+    last row, 14 doubles, one broadcast per rank: dh_gen_sweep), each rank prices its block, and
+    one gather brings the blocks (params, spots, noise, prices) to rank 0, which builds and saves
+    the reference output.  Bit for bit the single-process draw (synthetic_generator.py:98-141);
+    every rank's ``np.random`` ends where rank 0's draw leaves it.
 
 Only collectives on small host-side records and (generator) the price block are used; the COS
 kernels never wait on another rank.  The collectives run over ``torch.distributed`` (a process
@@ -57,18 +61,35 @@ def _world(group=None, comm=None):
     return dist.get_rank(group), dist.get_world_size(group)
 
 
-def _broadcast_f64(arr, shape, group=None, device=None, comm=None):
-    """Broadcast a float64 array from rank 0 (bit-exact)."""
+def _broadcast_f64(arr, shape, group=None, device=None, comm=None, root=0):
+    """Broadcast a float64 array from rank ``root`` (bit-exact)."""
     if comm is not None:
-        buf = (np.array(arr, dtype=np.float64).reshape(shape) if comm.rank == 0
+        buf = (np.array(arr, dtype=np.float64).reshape(shape) if comm.rank == root
                else np.zeros(shape))
-        return comm.broadcast(buf, 0)
+        return comm.broadcast(buf, root)
     dev = _comm_device(group, device)
     t = torch.empty(shape, dtype=torch.float64, device=dev)
-    if dist.get_rank(group) == 0:
+    if dist.get_rank(group) == root:
         t.copy_(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64).reshape(shape)))
-    dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    src = dist.get_global_rank(group, root) if group is not None else root
+    dist.broadcast(t, src=src, group=group)
     return t.cpu().numpy()
+
+
+def _gather_rows(block, group=None, device=None, comm=None):
+    """Rank 0 gets every rank's float64 block (same shape on every rank) as [world, *shape] in
+    rank order; other ranks get None (the native communicator all-gathers)."""
+    rank, world = _world(group, comm)
+    blk = np.ascontiguousarray(block, dtype=np.float64)
+    if comm is not None:
+        out = comm.allgather(blk)
+        return out if rank == 0 else None
+    dev = _comm_device(group, device)
+    mine = torch.from_numpy(blk).to(dev)
+    parts = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
+    dst = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.gather(mine, parts, dst=dst, group=group)
+    return np.stack([p.cpu().numpy() for p in parts]) if rank == 0 else None
 
 
 def start_shard(n_starts: int, rank: int, world: int):
@@ -220,12 +241,28 @@ def sample_block(n: int, rank: int, world: int):
     return lo, min(n, lo + per)
 
 
+def chunk_starts(n: int, world: int, chunk: int):
+    """The located chunk starts of every rank's block, in sample order: each block cut into
+    ``chunk``-sample chunks (the same list on every rank)."""
+    out = []
+    for r in range(world):
+        lo, hi = sample_block(n, r, world)
+        out.extend(range(lo, hi, chunk))
+    return np.array(out, dtype=np.int64)
+
+
+# what the last generate_sharded call did on this rank (instrumentation: samples this process
+# drew natively, its block, and the stages' seconds)
+last_generate_stats: dict = {}
+
+
 def generate_sharded(n_samples: int = 500,
                      save_path: str = "lbfgs_calibrations_synthetic.pkl", *, N: int = 128,
                      as_arrays: bool = False, verbose: bool = True, group=None, price_fn=None,
                      device=None, comm=None):
-    """``generate_synthetic_calibrations`` with the pricing sharded over the process group.
-    Rank 0 returns (and saves) the reference output; other ranks return None."""
+    """``generate_synthetic_calibrations`` with the draw and the pricing sharded over the process
+    group (module docstring).  Rank 0 returns (and saves) the reference output; other ranks return
+    None."""
     from . import generator as G
 
     rank, world = _world(group, comm)
@@ -235,31 +272,59 @@ def generate_sharded(n_samples: int = 500,
                                                  as_arrays=as_arrays, verbose=verbose)
     price_fn = price_fn or (lambda p, s: G.price_grid(p, s, N=N, device=device))
     n_opt = len(G.STRIKES_PCT) * len(G.MATURITIES)
-    # every rank draws the whole stream itself from rank 0's RNG state (627 words broadcast; the
-    # native draw is parallel on each rank's host threads), so no rank waits for rank 0's draw
-    # and nothing of the draws crosses the links; every rank's np.random ends where rank 0's
-    # draw leaves it
-    if world > 1 or comm is not None:
-        state = _rng_state_vec() if rank == 0 else None
-        _set_rng_state_vec(_broadcast_f64(state, (627,), group, device, comm))
-    params, spots, noise = G.draw_paths(n_samples)
-    lo, hi = sample_block(n_samples, rank, world)
-    block = price_fn(params[lo:hi], spots[lo:hi]) if hi > lo else np.empty((0, n_opt))
-    if world > 1 or comm is not None:
-        per = (n_samples + world - 1) // world
-        buf = np.zeros((per, n_opt))
-        buf[:hi - lo] = block
-        if comm is not None:
-            model = comm.allgather(buf).reshape(world * per, n_opt)[:n_samples]
-        else:
-            dev = _comm_device(group, device)
-            mine = torch.from_numpy(buf).to(dev)
-            parts = [torch.empty_like(mine) for _ in range(world)]
-            dist.all_gather(parts, mine, group=group)
-            model = np.concatenate([p.cpu().numpy() for p in parts])[:n_samples]
+    n = int(n_samples)
+    t0 = time.perf_counter()
+    drawn0 = _native.gen_drawn_samples()
+    lo, hi = sample_block(n, rank, world)
+    starts = chunk_starts(n, world, G.LOCATE_CHUNK)
+    # rank 0: the serial part of the draw (twister, acceptance bitmaps, walk), no sample drawn;
+    # every rank gets the states at all chunk starts and the state the whole draw leaves
+    shape = (starts.size + 1, _native.GEN_LOC_WORDS)
+    block = None
+    if rank == 0:
+        loc, end = G.locate_samples(_rng_state_vec(), n, starts, n_opt)
+        block = np.concatenate([loc, end[None, :]])
+    block = _broadcast_f64(block, shape, group, device, comm)
+    _set_rng_state_vec(block[-1])
+    t_loc = time.perf_counter()
+    mine = (starts >= lo) & (starts < hi)
+    if hi > lo:
+        params, spots, noise = G.draw_block(block[:-1][mine], starts[mine], hi, n_opt)
     else:
-        model = block
+        params, spots, noise = np.empty((0, 13)), np.empty(0), np.empty((0, n_opt))
+    t_draw = time.perf_counter()
+    # the AR(1) blend and the spot walk carry across blocks: rank r sweeps its block from rank
+    # r - 1's last row and hands its own last row on (a block that is empty passes it through)
+    carry = np.zeros(14)
+    for r in range(world):
+        if rank == r:
+            carry = G.sweep_block(params, spots, lo, carry)
+        if r < world - 1:
+            carry = _broadcast_f64(carry, (14,), group, device, comm, root=r)
+    t_sweep = time.perf_counter()
+    model = price_fn(params, spots) if hi > lo else np.empty((0, n_opt))
+    t_price = time.perf_counter()
+    # one gather: every block's params, spots, noise and prices to rank 0
+    per = (n + world - 1) // world
+    width = 13 + 1 + 2 * n_opt
+    buf = np.zeros((per, width))
+    buf[:hi - lo, :13], buf[:hi - lo, 13] = params, spots
+    buf[:hi - lo, 14:14 + n_opt], buf[:hi - lo, 14 + n_opt:] = noise, model
+    allb = _gather_rows(buf, group, device, comm)
+    t_gather = time.perf_counter()
+    last_generate_stats.clear()
+    last_generate_stats.update(
+        rank=rank, world=world, block=(lo, hi), samples=n,
+        samples_drawn=_native.gen_drawn_samples() - drawn0,
+        seconds={"locate_broadcast": t_loc - t0, "draw": t_draw - t_loc,
+                 "sweep_chain": t_sweep - t_draw, "price": t_price - t_sweep,
+                 "gather": t_gather - t_price})
     if rank != 0:
         return None
+    rows = allb.reshape(world * per, width)[:n]
+    params = np.ascontiguousarray(rows[:, :13])
+    spots = np.ascontiguousarray(rows[:, 13])
+    noise = np.ascontiguousarray(rows[:, 14:14 + n_opt])
+    model = np.ascontiguousarray(rows[:, 14 + n_opt:])
     return G.assemble(params, spots, noise, model, save_path, as_arrays=as_arrays,
                       verbose=verbose, N=N)

@@ -109,6 +109,37 @@ def draw_paths_async(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
     return _native.GenDraw(n_samples, lo, hi, n_opt, ALPHA, SPOT_BASE, 0.0003, 0.01, 0.02)
 
 
+# samples per located chunk of the sharded draw (a rank's chunks are drawn in parallel)
+LOCATE_CHUNK = 1 << 14
+
+
+def _ranges():
+    lo = np.array([v[0] for v in PARAM_RANGES.values()])
+    hi = np.array([v[1] for v in PARAM_RANGES.values()])
+    return lo, hi
+
+
+def locate_samples(state, n_samples, starts, n_opt=len(STRIKES_PCT) * len(MATURITIES)):
+    """The serial part of an n_samples draw from the np.random state ``state`` ([627]): the
+    generator's state at each sample index of ``starts`` (dh_gen_locate) -> (loc [n, 627], the
+    state the whole draw leaves [627]).  No sample is drawn."""
+    return _native.gen_locate(state, n_samples, n_opt, starts)
+
+
+def draw_block(loc, starts, i_end, n_opt=len(STRIKES_PCT) * len(MATURITIES)):
+    """Samples [starts[0], i_end) from their located chunk states (dh_gen_draw_located): (raw
+    params, spot returns, noise); sweep_block then applies the AR(1) blend and the spot walk."""
+    lo, hi = _ranges()
+    return _native.gen_draw_located(loc, starts, i_end, lo, hi, n_opt, 0.0003, 0.01, 0.02)
+
+
+def sweep_block(params, rets, i0, carry):
+    """AR(1) blend (:105-109) and spot walk (:112-116) of a drawn block of samples [i0, ...), in
+    place (rets become spots), from the previous sample's row ``carry`` [14] -> this block's last
+    row (dh_gen_sweep)."""
+    return _native.gen_sweep(params, rets, i0, ALPHA, SPOT_BASE, carry)
+
+
 def draw_paths_numpy(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
     """draw_paths as a per-sample NumPy loop (the reference's calls, vectorised per sample);
     kept as the tests' cross-check of the native draw."""

@@ -142,6 +142,59 @@ def test_sharded_equals_single_process(tmp_path, world, n_starts):
     assert b"lbfgs_calibrator" in raw and b"CalibrationResult" in raw
 
 
+def fake_price_fn(params, spots):
+    """A cheap deterministic stand-in for the pricer (what is under test is the partitioned draw,
+    the carry chain and the gather, not the prices): positive, row-dependent."""
+    return np.outer(spots, np.arange(1.0, 16.0)) * params[:, :1] + params[:, 1:2]
+
+
+def _gen_worker(rank, world, port, out_dir, n_samples):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    os.environ["DHCOS_GEN_THREADS"] = "4"          # two ranks share the container's 8 CPUs
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        np.random.seed(11 if rank == 0 else 500 + rank)   # only rank 0's state matters
+        np.random.random(3)
+        np.random.normal()                                # a cached gauss at entry
+        out = D.generate_sharded(n_samples, None, as_arrays=True, verbose=False,
+                                 price_fn=fake_price_fn)
+        stats = dict(D.last_generate_stats)
+        rng_after = np.random.random(4)
+        if rank == 0:
+            np.savez(os.path.join(out_dir, "gen.npz"),
+                     **{k: v for k, v in out.items() if k not in ("param_names", "risk_free")})
+        with open(os.path.join(out_dir, f"gstats{rank}.pkl"), "wb") as fh:
+            pickle.dump({"stats": stats, "rng": rng_after}, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_generate_sharded_partitions_the_draw(tmp_path):
+    """a gloo world-2 generate_sharded(1_000_000) equals the single process
+    bit for bit (every output array and the RNG continuation), and each rank draws at most 55%
+    of the samples (the library's own count of the samples this process drew): rank 0 only
+    locates the chunk starts of rank 1's block (twister, acceptance bitmaps, walk), it does not
+    draw them."""
+    n, world = 1_000_000, 2
+    mp.spawn(_gen_worker, args=(world, _free_port(), str(tmp_path), n), nprocs=world, join=True)
+    np.random.seed(11)
+    np.random.random(3)
+    np.random.normal()
+    p, s, nz = G.draw_paths(n)
+    want_rng = np.random.random(4)
+    want = G.assemble(p, s, nz, fake_price_fn(p, s), None, as_arrays=True, verbose=False)
+    got = np.load(tmp_path / "gen.npz")
+    for k in ("dates", "spot", "params", "market_prices", "model_prices", "strikes",
+              "maturities", "final_loss"):
+        assert np.array_equal(got[k], want[k]), k
+    for r in range(world):
+        g = pickle.load(open(tmp_path / f"gstats{r}.pkl", "rb"))
+        np.testing.assert_array_equal(g["rng"], want_rng)
+        lo, hi = g["stats"]["block"]
+        assert g["stats"]["samples_drawn"] == hi - lo <= 0.55 * n, g["stats"]
+
+
 def test_shard_helpers():
     assert D.start_shard(8, 1, 3) == [1, 4, 7]
     assert sorted(sum((D.start_shard(64, r, 8) for r in range(8)), [])) == list(range(64))

@@ -227,3 +227,92 @@ def test_parallel_draw_small_runs_repeated(monkeypatch):
         got = G.draw_paths(4096)
         for a, b in zip(got, want):
             assert np.array_equal(a, b)
+
+
+def _state_vec():
+    name, key, pos, hg, c = np.random.get_state()
+    return np.concatenate([np.asarray(key, dtype=np.float64), [pos, hg, c]])
+
+
+# (n, ranks, chunk, pre): empty and one-sample draws, blocks of one chunk, chunks of 7 samples
+# (cached gauss values carried across many chunk starts), ranks with empty blocks, a draw
+# straddling many generations, and the 16k-sample chunks generate_sharded uses
+@pytest.mark.parametrize("n,world,chunk,pre", [(0, 2, 7, 0), (1, 3, 7, 1), (2, 4, 1, 2),
+                                                (15, 2, 7, 1), (40, 4, 3, 3), (5000, 3, 7, 0),
+                                                (70001, 2, 1 << 14, 1), (70001, 5, 1000, 2)])
+def test_locate_draw_located_sweep_equal_the_draw(n, world, chunk, pre):
+    """The sharded draw's three pieces -- dh_gen_locate (one rank: twister, acceptance bitmaps,
+    walk; no sample drawn), dh_gen_draw_located (each rank its own chunks) and dh_gen_sweep (the
+    AR(1) blend and spot walk carried rank to rank) -- give dh_gen_draw's samples bit for bit,
+    and locate leaves np.random's state exactly where the draw leaves it."""
+    from dhcos import _native
+    from dhcos import distributed as D
+    np.random.seed(1000 + n)
+    np.random.random(pre)
+    for _ in range(pre % 2):
+        np.random.normal()
+    st = np.random.get_state()
+    want = G.draw_paths(n)
+    want_state = _state_vec()
+    np.random.set_state(st)
+    starts = D.chunk_starts(n, world, chunk)
+    drawn0 = _native.gen_drawn_samples()
+    loc, end = G.locate_samples(_state_vec(), n, starts)
+    assert _native.gen_drawn_samples() == drawn0          # locating draws nothing
+    assert np.array_equal(end, want_state)
+    carry, parts = np.zeros(14), []
+    for r in range(world):
+        lo, hi = D.sample_block(n, r, world)
+        m = (starts >= lo) & (starts < hi)
+        blk = G.draw_block(loc[m], starts[m], hi) if hi > lo else (
+            np.empty((0, 13)), np.empty(0), np.empty((0, 15)))
+        carry = G.sweep_block(blk[0], blk[1], lo, carry)
+        parts.append(blk)
+    assert _native.gen_drawn_samples() - drawn0 == n
+    for k in range(3):
+        assert np.array_equal(np.concatenate([p[k] for p in parts]), want[k]), k
+
+
+def test_located_states_are_numpy_states():
+    """A located state is np.random's own state at that sample: set into NumPy, its next draws
+    are the sample's uniforms and gauss values."""
+    np.random.seed(3)
+    np.random.normal()
+    st = np.random.get_state()
+    n, at = 200, np.array([0, 57, 199])
+    loc, _ = G.locate_samples(_state_vec(), n, at)
+    np.random.set_state(st)
+    lo, hi = G._ranges()
+    ref = G.draw_paths_numpy(n)
+    for j, i in enumerate(at):
+        np.random.set_state(("MT19937", loc[j, :624].astype(np.uint32), int(loc[j, 624]),
+                             int(loc[j, 625]), float(loc[j, 626])))
+        raw = np.random.uniform(lo, hi)
+        if i == 0:
+            assert np.array_equal(raw, ref[0][0])
+        else:                 # the blend: alpha prev + (1 - alpha) raw
+            assert np.array_equal(G.ALPHA * ref[0][i - 1] + (1 - G.ALPHA) * raw, ref[0][i])
+            np.random.normal(0.0003, 0.01)
+        assert np.array_equal(np.random.normal(0, 0.02, 15), ref[2][i])
+
+
+def test_sharded_draw_rejects_bad_arguments():
+    from dhcos import _native
+    st = np.zeros(627)
+    st[624] = 625                                         # pos outside [0, 624]
+    with pytest.raises(_native.NativeError):
+        _native.gen_locate(st, 10, 15, [0])
+    st[624] = 624
+    with pytest.raises(_native.NativeError):
+        _native.gen_locate(st, 10, 15, [5, 2])            # starts must not decrease
+    with pytest.raises(_native.NativeError):
+        _native.gen_locate(st, 10, 15, [11])              # past the draw
+    np.random.seed(0)
+    loc, _ = _native.gen_locate(_state_vec(), 10, 15, [0])
+    bad = loc.copy()
+    bad[0, 3] = 0.5                                       # a key word that is no uint32
+    lo, hi = G._ranges()
+    with pytest.raises(_native.NativeError):
+        _native.gen_draw_located(bad, [0], 10, lo, hi, 15, 0.0003, 0.01, 0.02)
+    with pytest.raises(_native.NativeError):
+        _native.gen_draw_located(loc, [0], -1, lo, hi, 15, 0.0003, 0.01, 0.02)
