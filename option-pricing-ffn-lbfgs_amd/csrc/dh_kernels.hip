@@ -33,6 +33,7 @@
 //   Validation ("exact") mode runs cos_exact_kernel instead: per-term CF + sincos in the
 //   reference's operation order, one wave per option.
 #include <hip/hip_runtime.h>
+#include <array>
 #include <rccl/rccl.h>   // types only: librccl is resolved at run time (dlopen)
 #include <dlfcn.h>
 
@@ -113,6 +114,14 @@ struct PriceArgs {
                             // formed by table_prologue_kernel ahead of it, else null
     double tail;            // tail_delta's scale: kTailScale, or -1 (dh_ctx_set_tail_cut(0): every
                             // term summed); set by launch_price
+    // prologues ahead (fused kernel, requests of more than one round of resident blocks): block
+    // q < ahead_stride forms the prologue constants of tables q + j ahead_stride (j = 1 ..
+    // kAheadMax) into ahead[.][kTabC] and then sets ahead_flag[.] = ahead_epoch; a later block
+    // whose flag holds this launch's epoch loads its constants instead of forming them
+    double* ahead;
+    unsigned* ahead_flag;
+    int ahead_stride;       // 0: off
+    unsigned ahead_epoch;
 };
 
 // w_k of table q sits at table_w(A, q)[k * table_step(A)].  The small-tile option kernel has one
@@ -634,6 +643,128 @@ __device__ __forceinline__ int cf_cut_group8(const dh::Params& P, double T, doub
         if (m) return (j0 + __ffs((int)m)) * st;               // j = j0 + ffs - 1, k = (j + 1) st
     }
     return N;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Prologues ahead (round 5).  A fused request of more than one round of resident blocks (C3:
+// 4,200 tables on 1,024 slots) spends ~18% of every block's chain, and ~1,000 wave-instructions
+// per table, on the serial prologue (table_prologue_wave + the CF-cut test).  Its first-round
+// blocks form the later-round tables' prologues on a wave that otherwise only stages a few
+// options before the first barrier: 8 lanes per table (the two variance factors on sub-lanes 0
+// and 1, the six exponentials on sub-lanes 0 .. 5: table_prologue_wave's expressions on the same
+// operands, uncontracted, so the same bits), the CF-cut candidates 8 at a time (cf_cut_group8:
+// the same first passing candidate as the wave's ballot).  The constants go out with agent-scope
+// stores; after the CF loop (the stores long drained: s_waitcnt vmcnt(0)) a flag per table takes
+// the launch's epoch -- MI355X_MICROARCH.md's "valid forms" row 1, as the loss hand-off.  A
+// later block reads its flag: set, it loads the 31 constants (wave 0 slots 0 .. 29, the cut wave
+// slot 30); not set (its writer has not got there: never seen, dispatch runs in block order and
+// a later block starts only after a whole block lifetime), it forms them itself.  Either way the
+// same values, so the same bits.
+// ----------------------------------------------------------------------------------------------
+constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane groups of a wave
+
+// v of lane (lane & ~7) | l: the 8-lane group's broadcast
+__device__ __forceinline__ double grp8_bcast(double v, int l) {
+    const int src = ((int)__lane_id() & ~7) | l;
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl((int)b, src, 64);
+    const int hi = __shfl((int)(b >> 32), src, 64);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ void agent_store(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The writer: block q0 (< ahead_stride) forms tables q0 + (j + 1) R, j = lane / 8, into ahead[]
+// (every lane of the wave calls this; groups past the grid form nothing)
+__device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead& H, int64_t q0,
+                                            int64_t nblocks, int lane) {
+#pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
+    const int sub = lane & 7;
+    const int64_t qa = q0 + (int64_t)((lane >> 3) + 1) * A.ahead_stride;
+    const bool act = qa < nblocks;
+    const int64_t q = act ? qa : q0;              // inactive groups run in step on a valid table
+    const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
+    const int g = (int)((unsigned)q % (unsigned)H.tpp);
+    const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
+    const double T = H.tsrc[H.paired ? p : g];
+    const bool two = sub & 1;                      // factor 2 on odd sub-lanes
+    const double v0 = two ? P.v02 : P.v01, k = two ? P.k2 : P.k1, th = two ? P.t2 : P.t1;
+    const double sg = two ? P.s2 : P.s1, rh = two ? P.r2 : P.r1;
+    double c1j, c2j;
+    dh::factor_cumulants(T, P.r, v0, k, th, sg, rh, c1j, c2j);   // double_heston.py:101-118
+    const double c1 = grp8_bcast(c1j, 0) + grp8_bcast(c1j, 1) + P.lam * T * P.muj;
+    const double c2 = grp8_bcast(c2j, 0) + grp8_bcast(c2j, 1) +
+                      P.lam * T * (P.sj * P.sj + P.muj * P.muj);
+    const double h = A.L * sqrt(fabs(c2));
+    const double a = c1 - h;                       // trunc_unclamped (double_heston.py:120-132)
+    const double b = c1 + h;
+    int2 gr = make_int2((int)p, 1);
+    if (!H.paired) gr = H.groups[g];
+    const dh::FactorC Fj = dh::factor_consts(v0, k, th, sg, rh);
+    const int e_lane = sub < 6 ? sub : 0;
+    const double arg = e_lane == 0 ? b : e_lane == 1 ? a : e_lane == 2 ? a + 0.1
+                     : e_lane == 3 ? b - 0.1 : e_lane == 4 ? P.muj + 0.5 * (P.sj * P.sj)
+                     : -P.r * T;
+    const double e = exp(arg);
+    dh::CfConsts CC;
+    double* f1 = (double*)&CC.f1;
+    double* f2 = (double*)&CC.f2;
+    const double* fj = (const double*)&Fj;
+    for (int i = 0; i < (int)(sizeof(dh::FactorC) / 8); ++i) {
+        f1[i] = grp8_bcast(fj[i], 0);
+        f2[i] = grp8_bcast(fj[i], 1);
+    }
+    const double comp = grp8_bcast(e, 4) - 1.0;    // cf_consts
+    CC.drift = (P.r - P.q - P.lam * comp) * T;
+    CC.half_sj2 = 0.5 * (P.sj * P.sj);
+    CC.muj = P.muj;
+    CC.lt = P.lam * T;
+    const double e0 = grp8_bcast(e, 0), e1 = grp8_bcast(e, 1), e2 = grp8_bcast(e, 2);
+    const double e3 = grp8_bcast(e, 3), e5 = grp8_bcast(e, 5);
+    const int kcf = cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, sub);
+    if (act && sub == 0) {
+        double* c = A.ahead + qa * kTabC;
+        agent_store(c + 0, a);
+        agent_store(c + 1, b);
+        agent_store(c + 2, e0);
+        agent_store(c + 3, e1);
+        agent_store(c + 4, 2.0 / (b - a));
+        agent_store(c + 5, dh::kPi / (b - a));
+        const double* cc = (const double*)&CC;
+        for (int i = 0; i < 16; ++i) agent_store(c + 6 + i, cc[i]);
+        agent_store(c + 22, P.S0);
+        agent_store(c + 23, P.r);
+        agent_store(c + 24, T);
+        agent_store(c + 25, e2 * (1.0 + kClampMargin));
+        agent_store(c + 26, e3 * (1.0 - kClampMargin));
+        agent_store(c + 27, gr.x);
+        agent_store(c + 28, gr.y);
+        agent_store(c + 29, e5);
+        agent_store(c + 30, kcf);
+    }
+}
+
+// The writer's flags, once its constant stores have drained (every lane of the wave calls this)
+__device__ __forceinline__ void ahead_publish(const PriceArgs& A, int64_t q0, int64_t nblocks,
+                                              int lane) {
+    const int64_t qa = q0 + (int64_t)((lane >> 3) + 1) * A.ahead_stride;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((lane & 7) == 0 && qa < nblocks)
+        __hip_atomic_store(&A.ahead_flag[qa], A.ahead_epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The reader: this launch's constants of table q are in ahead[] (a wave-uniform answer)
+__device__ __forceinline__ bool ahead_ready(const PriceArgs& A, int64_t q) {
+    const unsigned f = __hip_atomic_load(&A.ahead_flag[q], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(f) == A.ahead_epoch;
+}
+
+__device__ __forceinline__ double agent_load(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Every table's prologue of a large fused request ahead of the fused launch (launch_fused): the
@@ -1854,14 +1985,31 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // (the <= 96-VGPR wide build runs it on wave 0 after the prologue: one range computation
     // less, and the build's register allocation gains: C4 -2.6%)
     const int wcut = (nthr > 64 && WV <= DH_FUSED_WAVES) ? nthr / 64 - 1 : 0;
-    if (!H.pre && (wv == 0 || wv == wcut)) serial_prio(true);
+    // prologues ahead (4-wave build, >= 3 waves): the first-round block's writer wave, and
+    // whether this block's constants may have been formed ahead
+    const int64_t R = (WV <= DH_FUSED_WAVES && nthr >= 192) ? A.ahead_stride : 0;
+    const int wahead = nthr / 64 - 2;
+    const bool ahead_w = R > 0 && q < R;
+    const bool ahead_r = R > 0 && q >= R && q < (kAheadMax + 1) * R;
+    const int64_t nblocks = gridDim.x;
+    if (!H.pre && (wv == 0 || wv == wcut || (ahead_w && wv == wahead))) serial_prio(true);
     if (H.pre) {
         if (t < kTabC) shc[t] = H.pre[q * kTabC + t];
     } else if (wv == 0) {
-        table_prologue_wave(A, H, q, shc, lane, wcut == 0);
+        // (each of the two waves decides on its own flag load and fills its own slots: loaded or
+        // formed, the same values, so a flag set between the two loads changes nothing)
+        if (ahead_r && ahead_ready(A, q)) {
+            if (lane < (wcut == 0 ? kTabC : 30)) shc[lane] = agent_load(A.ahead + q * kTabC + lane);
+        } else {
+            table_prologue_wave(A, H, q, shc, lane, wcut == 0);
+        }
     } else if (wv == wcut) {
-        const int kcf = A.N < kCfCutMinN ? A.N : prologue_cut_wave(A, H, q, lane);
-        if (lane == 0) shc[30] = kcf;
+        if (ahead_r && ahead_ready(A, q)) {
+            if (lane == 0) shc[30] = agent_load(A.ahead + q * kTabC + 30);
+        } else {
+            const int kcf = A.N < kCfCutMinN ? A.N : prologue_cut_wave(A, H, q, lane);
+            if (lane == 0) shc[30] = kcf;
+        }
     }
     DH_STAMP(A, 8);
     const int N = A.N;
@@ -1892,6 +2040,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         L.xK[i] = xK;
         L.exK[i] = ratio;
     }
+    if (ahead_w && wv == wahead) ahead_write(A, H, q, nblocks, lane);
     __syncthreads();
     serial_prio(false);
     if (__builtin_amdgcn_readfirstlane(live_v) <= 0) return;   // every block reads the same count
@@ -1974,6 +2123,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP_T(A, 17, 128);
         DH_STAMP_T(A, 18, 192);
     }
+    if (ahead_w && wv == wahead) ahead_publish(A, q, nblocks, lane);
     if constexpr (!kEarlyClamp) clamp_scan();
     DH_STAMP(A, 21);
     DH_STAMP_T(A, 22, 64);
@@ -2336,6 +2486,14 @@ struct dh_ctx {
     int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
     DevBuf stamps;
     int64_t stamps_n = 0;
+    // prologues ahead (launch_fused): constants and flags of the later-round tables, the launch
+    // epoch, $DHCOS_AHEAD (-1: not read yet; 0 turns it off) and the resident-block counts of the
+    // fused kernel builds it applies to, by (t1, r1, LDS bytes)
+    DevBuf ahead, ahead_flag;
+    size_t ahead_flag_cap = 0;
+    unsigned ahead_epoch = 0;
+    int ahead_on = -1;
+    std::vector<std::pair<std::array<int64_t, 3>, int>> resident_fused;
 };
 
 struct dh_surface {
@@ -2508,6 +2666,52 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     const dim3 grid((unsigned)blocks), block((unsigned)std::max(t1, t2));
     const double* tsrc = A.paired ? A.T : A.group_T;       // FusedHead: preloaded arguments
     const bool r1 = tile_r(max_nopt, t2) == 1;
+    A.ahead = nullptr;
+    A.ahead_flag = nullptr;
+    A.ahead_stride = 0;
+    if (ctx->ahead_on < 0) {
+        const char* e = std::getenv("DHCOS_AHEAD");
+        ctx->ahead_on = (e && e[0] == '0') ? 0 : 1;
+    }
+    // prologues ahead: the 4-wave build of >= 3-wave blocks, more blocks than one round of
+    // resident ones, in-block prologues (no prologue kernel)
+    const bool wide = r1 && blocks >= kFusedWideMinBlocks;
+    if (ctx->ahead_on && !wide && block.x >= 192 && blocks < kPrologueKernelMinBlocks &&
+        !ctx->stamps_on) {
+        const std::array<int64_t, 3> key{t1, r1 ? 1 : 0, (int64_t)lds};
+        int res = -1;
+        for (const auto& kv : ctx->resident_fused)
+            if (kv.first == key) res = kv.second;
+        if (res < 0) {
+            const void* f = nullptr;
+            switch (t1 * (r1 ? 1 : -1)) {
+                case 64: f = (const void*)cos_fused_kernel<64, 1>; break;
+                case 128: f = (const void*)cos_fused_kernel<128, 1>; break;
+                case 256: f = (const void*)cos_fused_kernel<256, 1>; break;
+                case -64: f = (const void*)cos_fused_kernel<64, kR>; break;
+                case -128: f = (const void*)cos_fused_kernel<128, kR>; break;
+                default: f = (const void*)cos_fused_kernel<256, kR>; break;
+            }
+            int per_cu = 0, cus = 0;
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, (int)block.x, lds));
+            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+            res = std::max(1, per_cu) * std::max(1, cus);
+            ctx->resident_fused.push_back({key, res});
+        }
+        if (blocks > res) {
+            HIP_TRY(ctx->ahead.reserve((size_t)blocks * kTabC * sizeof(double)));
+            if ((size_t)blocks > ctx->ahead_flag_cap) {
+                HIP_TRY(ctx->ahead_flag.reserve((size_t)blocks * sizeof(unsigned)));
+                HIP_TRY(hipMemsetAsync(ctx->ahead_flag.ptr, 0, ctx->ahead_flag.cap, st));
+                ctx->ahead_flag_cap = ctx->ahead_flag.cap / sizeof(unsigned);
+            }
+            if (++ctx->ahead_epoch == 0) ++ctx->ahead_epoch;     // 0: the cleared flags' value
+            A.ahead = (double*)ctx->ahead.ptr;
+            A.ahead_flag = (unsigned*)ctx->ahead_flag.ptr;
+            A.ahead_stride = res;
+            A.ahead_epoch = ctx->ahead_epoch;
+        }
+    }
     if (blocks >= kPrologueKernelMinBlocks && !ctx->stamps_on) {
         HIP_TRY(ctx->pre.reserve((size_t)blocks * kTabC * sizeof(double)));
         A.pre = (const double*)ctx->pre.ptr;

@@ -173,6 +173,45 @@ def price_vec(prm, S0, K, T, r, is_call, N=128, q=0.0):
     return np.exp(-r * T) * np.sum(terms)
 
 
+def price_surface(prm, S0, K, T, r, is_call, N=128, q=0.0):
+    """price_vec for every option of a surface under one parameter set, as [M, N] arrays (the
+    fixture generators' fast checker for 1,024-option calibrations): per option the same
+    expressions as price_vec, broadcast over the options (tests/test_oracle_golden.py holds it
+    to price_vec at 1e-13)."""
+    K = np.asarray(K, dtype=np.float64).reshape(-1)
+    T = np.asarray(T, dtype=np.float64).reshape(-1)
+    call = np.broadcast_to(np.asarray(is_call, dtype=bool), K.shape)
+    xK = np.log(K / S0)
+    v01, k1, t1, s1, r1, v02, k2, t2, s2, r2, lam, muj, sj = prm
+    c1a, c2a = _factor_cumulants(T, r, v01, k1, t1, s1, r1)       # trunc_range, per option
+    c1b, c2b = _factor_cumulants(T, r, v02, k2, t2, s2, r2)
+    c1 = c1a + c1b + lam * T * muj
+    c2 = c2a + c2b + lam * T * (sj ** 2 + muj ** 2)
+    half = 10.0 * np.sqrt(np.abs(c2))
+    a = np.minimum(c1 - half, xK - 0.1)
+    b = np.maximum(c1 + half, xK + 0.1)
+    k = np.arange(N, dtype=np.float64)[None, :]
+    u = k * np.pi / (b - a)[:, None]
+    phi = cf(u, T[:, None], prm, r, q)
+    c = np.where(call, xK, a)[:, None]
+    d = np.where(call, b, xK)[:, None]
+    A = a[:, None]
+    ed, ec = np.exp(d), np.exp(c)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        cd, cc = np.cos(u * (d - A)), np.cos(u * (c - A))
+        sd, sc = np.sin(u * (d - A)), np.sin(u * (c - A))
+        ch = (1.0 / (1 + u ** 2)) * (cd * ed - cc * ec + u * sd * ed - u * sc * ec)
+        ps = (1.0 / u) * (sd - sc)
+    ch[:, 0] = (ed - ec)[:, 0]
+    ps[:, 0] = (d - c)[:, 0]
+    scale = (2.0 / (b - a))[:, None]
+    Kc = K[:, None]
+    V = np.where(call[:, None], scale * (S0 * ch - Kc * ps), scale * (Kc * ps - S0 * ch))
+    terms = np.real(phi * np.exp(-1j * u * A)) * V
+    terms[:, 0] *= 0.5
+    return np.exp(-r * T) * np.sum(terms, axis=1)
+
+
 def price_many(params, S0, K, T, r, is_call, N=128, q=0.0, scalar=False):
     """Loop helper: arrays broadcast over options; returns an ndarray of prices."""
     params = np.atleast_2d(np.asarray(params, dtype=np.float64))

@@ -905,10 +905,11 @@ def _with_path(ctx, path, fn):
                                  # fused path its 5-wave build (grids of >= 4,096 blocks)
     (49, 288, 1024, 32, 256),    # 9,216 tables: the fused blocks load their prologue constants
                                  # from table_prologue_kernel (grids of >= 8,192 blocks)
-    (50, 7, 2000, 20, 512),      # C3-like, odd param-set count: the multi-table kernel's last
-                                 # block of each group holds one table
-    (51, 43, 10000, 100, 512),   # C3 shape at 43 sets: 4,300 tables (AUTO takes the multi-table
-                                 # kernel), clamp-widened strikes in the first group
+    (50, 7, 2000, 20, 512),      # C3-like, odd param-set count
+    (51, 43, 10000, 100, 512),   # C3 shape at 43 sets: 4,300 tables, more than one round of
+                                 # resident blocks (the later rounds' prologue constants formed
+                                 # ahead by the first round's blocks), clamp-widened strikes in
+                                 # the first group
 ])
 def test_fused_equals_split_bitwise(dh, seed, P, M, n_T, N):
     """The fused single-launch request kernel and the table + option launches compute every
