@@ -1,20 +1,29 @@
 #!/usr/bin/env python3
-"""Generate tests/golden/calib_c2_single_start.json: the reference algorithm's single-start
-calibration (configs[1] of BASELINE.json as stated: calibrate(300, 1)) on the bench's C2 surface,
-the 1,024-option synthetic market (32 K/S x 32 T) at N = 256.
+"""Generate the C2-surface calibration fixtures: the reference algorithm's single-start
+calibration on bench.py's 1,024-option C2 surface (32 K/S x 32 T) at N = 256.
+
+  --start 0 (default) -> tests/golden/calib_c2_single_start.json: calibrate(300, 1) as configs[1]
+      of BASELINE.json states it, from the literature guess (start 0, which draws no random
+      numbers).  That start sits on the Feller kink: every member ends ABNORMAL at nit 0 after 21
+      requests (round 4).
+  --start 1 -> tests/golden/calib_c2_start1.json: calibrate(300, 1, x0=...) from start 1 of
+      calibrate(300, 3) under np.random.seed(0) (guess type 1, a draw of the global RNG): a start
+      that iterates (VERDICT r4 "missing" 3).
 
 Test infrastructure.  The market is built as bench.py make_surface(32, 32, N=256) builds it, but
 priced by the oracle (oracle/dh_oracle.py, the reference's pricer restated; its vectorised form,
 within ~1e-13 of the reference): model prices at a seed-1 draw of the generator's ranges, times
-(1 + N(0, 0.02)) with seed 2, calls, S0 = 100, r = 0.03.  The start is the calibrator's
-get_initial_guess(0) on that market (a NumPy restatement of lbfgs_calibrator.py:179-234, checked
-against the reference's own draws in tests/golden/calib.json).  The losses are the oracle's at
-N = 256, driven by scipy.optimize.minimize exactly as lbfgs_calibrator.py:259-269 calls it (the
-2-point forward difference SciPy forms, h = 1e-8).  Members 1-2 multiply every price by
-(1 + 1e-13 U(-1, 1)) (the scale of the GPU's own price differences), so the test can tell an
-outcome that depends on last bits from one that does not.
+(1 + N(0, 0.02)) with seed 2, calls, S0 = 100, r = 0.03.  The start comes from
+golden_common.pinned_start_points (a restatement of lbfgs_calibrator.py:179-234 checked against
+the reference's own draws in tests/golden/calib.json, and against the calibrator).  The losses are
+the oracle's at N = 256 (oracle.price_surface: price_vec's bits over the whole market), driven by
+scipy.optimize.minimize exactly as lbfgs_calibrator.py:259-269 calls it (the 2-point forward
+difference SciPy forms, h = 1e-8).  Member 0 is noise-free; members 1.. multiply every price by
+(1 + eps U(-1, 1)), eps = the GPU's measured relative price difference from the reference's
+pricer on this surface (tests/golden/gpu_price_noise.json, measure_price_noise.py), so the ensemble
+spans the outcomes that depend on last bits.
 
-Usage:  python tests/golden/make_calib_c2.py [--procs 3]     (~5 min of CPU per member)
+Usage:  python tests/golden/make_calib_c2.py [--start 1] [--members 8] [--procs 8]
 """
 import argparse
 import json
@@ -23,11 +32,10 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-from oracle import dh_oracle as O  # noqa: E402
-from make_calib_noise import GEN_HI, GEN_LO, run_start  # noqa: E402
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from golden_common import ROOT, O, pinned_start_points  # noqa: E402
+from make_calib_noise import GEN_HI, GEN_LO, measured_eps, run_start  # noqa: E402
 
 N = 256
 
@@ -44,32 +52,41 @@ def surface_c2():
 
 
 def _member(args):
-    market, x0, m, S0, r = args
-    eps = 0.0 if m == 0 else 1e-13
-    return dict(run_start(market, np.array(x0), eps, 7000 + m, scalar=False, S0=S0, r=r, N=N),
-                eps=eps)
+    market, x0, m, S0, r, eps = args
+    e = 0.0 if m == 0 else eps
+    return dict(run_start(market, np.array(x0), e, 7000 + m, S0=S0, r=r, N=N, surface=True),
+                eps=e)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--members", type=int, default=3)
-    ap.add_argument("--procs", type=int, default=3)
+    ap.add_argument("--start", type=int, default=0, choices=[0, 1])
+    ap.add_argument("--members", type=int, default=8)
+    ap.add_argument("--procs", type=int, default=8)
+    ap.add_argument("--eps", type=float, default=None,
+                    help="member noise scale (default: the measured C2 max, gpu_price_noise.json)")
     a = ap.parse_args()
     import multiprocessing as mp
     sys.path.insert(0, os.path.join(ROOT, "option-pricing-ffn-lbfgs_amd"))
-    from dhcos.calibrator import DoubleHestonJumpCalibrator   # get_initial_guess: NumPy only
+    from dhcos.calibrator import DoubleHestonJumpCalibrator   # start_points: NumPy only
     market, S0, r = surface_c2()
-    np.random.seed(0)
-    x0 = DoubleHestonJumpCalibrator(S0, r, market, N=N).start_points(1)[0].tolist()
+    x0 = pinned_start_points(DoubleHestonJumpCalibrator(S0, r, market, N=N), 3)[a.start].tolist()
+    eps, eps_src = (a.eps, "--eps") if a.eps is not None else measured_eps("c2")
     with mp.get_context("fork").Pool(a.procs) as pool:
-        members = pool.map(_member, [(market, x0, m, S0, r) for m in range(a.members)])
+        members = pool.map(_member, [(market, x0, m, S0, r, eps) for m in range(a.members)])
     for m, mb in enumerate(members):
         print(m, mb, flush=True)
-    out = {"what": "calibrate(300, 1) of the reference algorithm (oracle losses at N = 256, SciPy "
-                   "L-BFGS-B) on bench.py's C2 surface priced by the oracle, np.random.seed(0) "
-                   "start; member 0 noise-free, members 1.. prices x (1 + 1e-13 U(-1, 1))",
-           "N": N, "market": market, "S0": S0, "r": r, "x0": x0, "members": members}
-    with open(os.path.join(ROOT, "tests", "golden", "calib_c2_single_start.json"), "w") as fh:
+    funs = [mb["fun"] for mb in members]
+    name = "calib_c2_single_start.json" if a.start == 0 else "calib_c2_start1.json"
+    out = {"what": f"calibrate(300, 1) of the reference algorithm (oracle losses at N = 256, "
+                   f"SciPy L-BFGS-B) on bench.py's C2 surface priced by the oracle, from start "
+                   f"{a.start} of calibrate(300, 3) under np.random.seed(0); member 0 noise-free, "
+                   f"members 1.. prices x (1 + eps U(-1, 1)), eps = {eps:.3e} ({eps_src})",
+           "N": N, "market": market, "S0": S0, "r": r, "x0": x0, "start": a.start, "eps": eps,
+           "members": members, "fun_min": min(funs), "fun_max": max(funs),
+           "nit_min": min(mb["nit"] for mb in members),
+           "nit_max": max(mb["nit"] for mb in members)}
+    with open(os.path.join(HERE, name), "w") as fh:
         json.dump(out, fh, indent=1)
 
 

@@ -35,7 +35,11 @@ sys.path.insert(0, ROOT)
 from oracle import dh_oracle as O  # noqa: E402
 
 
-def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05, N=128):
+def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05, N=128, surface=False):
+    """One start of the reference algorithm: SciPy's L-BFGS-B on the oracle's losses at SciPy's
+    14 FD points per request, every price times (1 + eps U(-1, 1)) (seeded).  scalar: the
+    reference's per-option pricer (bitwise its prices); surface: oracle.price_surface (price_vec's
+    arithmetic over the whole market at once, the same bits: tests/test_oracle_golden.py)."""
     mk = np.array([o["price"] for o in market])
     K = [o["strike"] for o in market]
     T = [o["maturity"] for o in market]
@@ -44,7 +48,9 @@ def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05, N=128):
 
     def loss(x):
         p = O.to_params(x)
-        pr = O.price_many(p, S0, K, T, r, call, N, scalar=scalar)
+        with np.errstate(all="ignore"):
+            pr = (O.price_surface(p, S0, K, T, r, call, N) if surface
+                  else O.price_many(p, S0, K, T, r, call, N, scalar=scalar))
         if eps:
             pr = pr * (1 + eps * rs.uniform(-1, 1, pr.size))
         if not np.all(np.isfinite(pr)) or np.any(pr <= 0):
@@ -61,6 +67,16 @@ def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05, N=128):
                        options={"maxiter": 300, "ftol": 1e-9, "gtol": 1e-6, "maxfun": 15000 // 14})
     return {"fun": float(res.fun), "nit": int(res.nit), "nfev_requests": int(res.nfev),
             "message": str(res.message), "success": bool(res.success)}
+
+
+def measured_eps(name):
+    """The GPU's measured max relative price difference from the reference's pricer on surface
+    ``name`` (tests/golden/gpu_price_noise.json, measure_price_noise.py run on the GPU box) ->
+    (eps, where it came from)."""
+    path = os.path.join(ROOT, "tests", "golden", "gpu_price_noise.json")
+    with open(path) as fh:
+        g = json.load(fh)
+    return float(g[name]["max_rel"]), f"gpu_price_noise.json [{name}] max_rel"
 
 
 GEN_LO = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
@@ -80,10 +96,10 @@ def surface_5x5():
 
 
 def _member(args):
-    market, x0s, m, S0, r = args
-    # members 1-11: last-bit noise (1e-15); 12-23: the scale the GPU's own price differences
-    # reach on this surface (~1e-13 relative: the fast path's recurrence and summation order)
-    eps = 0.0 if m == 0 else (1e-15 if m < 12 else 1e-13)
+    market, x0s, m, S0, r, eps_m = args
+    # member 0: the reference-exact scalar pricer, noise-free; the others: the GPU's measured
+    # price differences on this surface as noise
+    eps = 0.0 if m == 0 else eps_m
     starts = [run_start(market, np.array(x0), eps, 1000 * m + s, scalar=(m == 0), S0=S0, r=r)
               for s, x0 in enumerate(x0s)]
     best, best_loss = None, np.inf
@@ -95,24 +111,33 @@ def _member(args):
             "iterations": starts[best]["nit"]}
 
 
+HISTORY = ("round 4: members at 1e-15 only; the GPU's start 2 on the 5 x 5 surface then ended "
+           "CONVERGENCE where all of them ended ABNORMAL (gpurun_out/t_mt.log), and 12 members at "
+           "1e-13 were added after that run.  Round 5: every member at the GPU's measured max "
+           "relative price difference from the reference's pricer on the surface "
+           "(gpu_price_noise.json, measure_price_noise.py), no scale chosen after a GPU result")
+
+
 def main_surface(members_n, procs):
     import multiprocessing as mp
     sys.path.insert(0, os.path.join(ROOT, "option-pricing-ffn-lbfgs_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     from dhcos.calibrator import DoubleHestonJumpCalibrator   # get_initial_guess: NumPy only
+    from golden_common import pinned_start_points
     market, S0, r = surface_5x5()
-    np.random.seed(0)
-    x0s = [x.tolist() for x in DoubleHestonJumpCalibrator(S0, r, market).start_points(3)]
+    x0s = [x.tolist() for x in pinned_start_points(DoubleHestonJumpCalibrator(S0, r, market), 3)]
+    eps, src = measured_eps("5x5")
     with mp.get_context("fork").Pool(procs) as pool:
-        members = pool.map(_member, [(market, x0s, m, S0, r) for m in range(members_n)])
+        members = pool.map(_member, [(market, x0s, m, S0, r, eps) for m in range(members_n)])
     for m, mb in enumerate(members):
         print(m, mb["best_start"], mb["final_loss"], mb["iterations"], mb["message"],
               [(s["nit"], s["message"][:12], round(s["fun"], 12)) for s in mb["starts"]])
     winners = [m["final_loss"] for m in members]
     out = {"what": "calibrate(300, 3) of the reference algorithm (oracle losses at N = 128, SciPy "
                    "L-BFGS-B) on a 5 x 5 synthetic surface (make_calib_noise.py surface_5x5), "
-                   "np.random.seed(0) starts, prices x (1 + eps U(-1, 1)) per member, eps = 1e-15 "
-                   "(members 1-11) or 1e-13 (members 12-23, the scale of the GPU's own price "
-                   "differences); member 0: the reference-exact scalar pricer, noise-free",
+                   f"np.random.seed(0) starts, prices x (1 + eps U(-1, 1)) per member, eps = "
+                   f"{eps:.3e} ({src}); member 0: the reference-exact scalar pricer, noise-free",
+           "history": HISTORY, "eps": eps,
            "market": market, "S0": S0, "r": r, "x0s": x0s,
            "members": members, "final_loss_min": min(winners), "final_loss_max": max(winners)}
     with open(os.path.join(ROOT, "tests", "golden", "calib_noise_5x5.json"), "w") as fh:
@@ -130,26 +155,23 @@ def main():
     with open(os.path.join(ROOT, "tests", "golden", "calib.json")) as fh:
         g = json.load(fh)
     market = g["test_market"]
-    x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
-    members = []
-    for m in range(a.members):
-        eps = 0.0 if m == 0 else 1e-15
-        starts = [run_start(market, x0, eps, 1000 * m + s, scalar=(m == 0))
-                  for s, x0 in enumerate(x0s)]
-        best, best_loss = None, np.inf
-        for s, st in enumerate(starts):          # lbfgs_calibrator.py:271: strict <, start order
-            if st["fun"] < best_loss:
-                best, best_loss = s, st["fun"]
-        members.append({"eps": eps, "pricer": "scalar" if m == 0 else "vectorised",
-                        "starts": starts, "best_start": best,
-                        "final_loss": best_loss, "message": starts[best]["message"],
-                        "iterations": starts[best]["nit"]})
-        print(m, best, best_loss, starts[best]["nit"], starts[best]["message"],
-              [(s["nit"], round(s["fun"], 12)) for s in starts], flush=True)
+    x0s = [s["x0"] for s in g["calibrate_seed0_starts"]]
+    eps, src = measured_eps("test_market")
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(a.procs) as pool:
+        members = pool.map(_member, [(market, x0s, m, 100.0, 0.05, eps)
+                                     for m in range(a.members)])
+    for m, mb in enumerate(members):
+        print(m, mb["best_start"], mb["final_loss"], mb["iterations"], mb["message"],
+              [(s["nit"], round(s["fun"], 12)) for s in mb["starts"]], flush=True)
     winners = [m["final_loss"] for m in members]
     out = {"what": "calibrate(300, 3) of the reference algorithm (oracle losses, SciPy L-BFGS-B) "
-                   "on tests/test_suite.py's market, np.random.seed(0) starts, prices x (1 + 1e-15 "
-                   "U(-1, 1)) per member (member 0: the reference-exact scalar pricer, noise-free)",
+                   "on tests/test_suite.py's market, np.random.seed(0) starts (the reference's own "
+                   f"draws, calib.json), prices x (1 + eps U(-1, 1)) per member, eps = {eps:.3e} "
+                   f"({src}); member 0: the reference-exact scalar pricer, noise-free",
+           "history": "round 3-4: members at 1e-15.  Round 5: every member at the GPU's measured "
+                      "max relative price difference on this market (gpu_price_noise.json)",
+           "eps": eps,
            "members": members, "final_loss_min": min(winners), "final_loss_max": max(winners)}
     with open(os.path.join(ROOT, "tests", "golden", "calib_noise.json"), "w") as fh:
         json.dump(out, fh, indent=1)
