@@ -676,15 +676,25 @@ __device__ __forceinline__ void agent_store(double* p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The writer: block q0 (< ahead_stride) forms tables q0 + (j + 1) R, j = lane / 8, into ahead[]
-// (every lane of the wave calls this; groups past the grid form nothing)
+// The later table of 8-lane group lane / 8 of first-round block q0: q0 + (j + 1) R (act: it
+// exists; an inactive group runs in step on q0's own table and stores nothing)
+__device__ __forceinline__ int64_t ahead_table(const PriceArgs& A, int64_t q0, int64_t nblocks,
+                                               int lane, bool& act) {
+    const int64_t qa = q0 + (int64_t)((lane >> 3) + 1) * A.ahead_stride;
+    act = qa < nblocks;
+    return act ? qa : q0;
+}
+
+// The writer (the staging wave, before the first barrier): tables q0 + (j + 1) R, j = lane / 8,
+// slots 0 .. 29 into ahead[]; each group's truncation range into ab[j] for the cut wave, which
+// forms slot 30 (K_cf) during the CF loop (ahead_cut)
 __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead& H, int64_t q0,
-                                            int64_t nblocks, int lane) {
+                                            int64_t nblocks, int lane, double (*ab)[2]) {
 #pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
     const int sub = lane & 7;
-    const int64_t qa = q0 + (int64_t)((lane >> 3) + 1) * A.ahead_stride;
-    const bool act = qa < nblocks;
-    const int64_t q = act ? qa : q0;              // inactive groups run in step on a valid table
+    bool act;
+    const int64_t q = ahead_table(A, q0, nblocks, lane, act);
+    const int64_t qa = q;
     const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
     const int g = (int)((unsigned)q % (unsigned)H.tpp);
     const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
@@ -723,7 +733,10 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
     CC.lt = P.lam * T;
     const double e0 = grp8_bcast(e, 0), e1 = grp8_bcast(e, 1), e2 = grp8_bcast(e, 2);
     const double e3 = grp8_bcast(e, 3), e5 = grp8_bcast(e, 5);
-    const int kcf = cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, sub);
+    if (sub == 0) {
+        ab[lane >> 3][0] = a;
+        ab[lane >> 3][1] = b;
+    }
     if (act && sub == 0) {
         double* c = A.ahead + qa * kTabC;
         agent_store(c + 0, a);
@@ -742,16 +755,35 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
         agent_store(c + 27, gr.x);
         agent_store(c + 28, gr.y);
         agent_store(c + 29, e5);
-        agent_store(c + 30, kcf);
     }
 }
 
-// The writer's flags, once its constant stores have drained (every lane of the wave calls this)
+// The cut wave's part (after its own K_cf, during the CF loop, which leaves it idle up to
+// K_cf = 192): each group's K_cf by cf_cut_group8 on the writer's range (the same first passing
+// candidate as the wave's ballot), into slot 30; then its stores drained.
+__device__ __forceinline__ void ahead_cut(const PriceArgs& A, const FusedHead& H, int64_t q0,
+                                          int64_t nblocks, int lane, const double (*ab)[2]) {
+    bool act;
+    const int64_t q = ahead_table(A, q0, nblocks, lane, act);
+    const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
+    const int g = (int)((unsigned)q % (unsigned)H.tpp);
+    const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
+    const double T = H.tsrc[H.paired ? p : g];
+    const double a = ab[lane >> 3][0], b = ab[lane >> 3][1];
+    const int kcf = A.N < kCfCutMinN
+                        ? A.N
+                        : cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N,
+                                        lane & 7);
+    if (act && (lane & 7) == 0) agent_store(A.ahead + q * kTabC + 30, kcf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The flags, after both waves' stores drained and a barrier (every lane of a wave calls this)
 __device__ __forceinline__ void ahead_publish(const PriceArgs& A, int64_t q0, int64_t nblocks,
                                               int lane) {
-    const int64_t qa = q0 + (int64_t)((lane >> 3) + 1) * A.ahead_stride;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if ((lane & 7) == 0 && qa < nblocks)
+    bool act;
+    const int64_t qa = ahead_table(A, q0, nblocks, lane, act);
+    if ((lane & 7) == 0 && act)
         __hip_atomic_store(&A.ahead_flag[qa], A.ahead_epoch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1967,6 +1999,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     __shared__ double red[4][1];
     __shared__ double2 sct[dh::kMathTab];
     __shared__ unsigned long long cmask[kTileMax / 64];
+    __shared__ double ahd_ab[kAheadMax][2];            // prologues ahead: later tables' ranges
     const int nthr = blockDim.x;
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -2040,7 +2073,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         L.xK[i] = xK;
         L.exK[i] = ratio;
     }
-    if (ahead_w && wv == wahead) ahead_write(A, H, q, nblocks, lane);
+    if (ahead_w && wv == wahead) ahead_write(A, H, q, nblocks, lane, ahd_ab);
     __syncthreads();
     serial_prio(false);
     if (__builtin_amdgcn_readfirstlane(live_v) <= 0) return;   // every block reads the same count
@@ -2123,12 +2156,16 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP_T(A, 17, 128);
         DH_STAMP_T(A, 18, 192);
     }
-    if (ahead_w && wv == wahead) ahead_publish(A, q, nblocks, lane);
+    // prologues ahead: the later tables' K_cf on the cut wave; both writer waves' stores drained
+    // before the barrier, the flags after it
+    if (ahead_w && wv == wcut) ahead_cut(A, H, q, nblocks, lane, ahd_ab);
+    if (ahead_w && wv == wahead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (!kEarlyClamp) clamp_scan();
     DH_STAMP(A, 21);
     DH_STAMP_T(A, 22, 64);
     __syncthreads();
     DH_STAMP(A, 2);
+    if (ahead_w && wv == wahead) ahead_publish(A, q, nblocks, lane);
 
     // ---- k-sums in the canonical order of a 64-thread table slot (from the LDS table; the same
     //      bits as cos_table_kernel).  c1 is a sum of zeros (+0.0) and w0 has one nonzero term
@@ -2676,8 +2713,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     // prologues ahead: the 4-wave build of >= 3-wave blocks, more blocks than one round of
     // resident ones, in-block prologues (no prologue kernel)
     const bool wide = r1 && blocks >= kFusedWideMinBlocks;
-    if (ctx->ahead_on && !wide && block.x >= 192 && blocks < kPrologueKernelMinBlocks &&
-        !ctx->stamps_on) {
+    if (ctx->ahead_on && !wide && block.x >= 192 && blocks < kPrologueKernelMinBlocks) {
         const std::array<int64_t, 3> key{t1, r1 ? 1 : 0, (int64_t)lds};
         int res = -1;
         for (const auto& kv : ctx->resident_fused)
