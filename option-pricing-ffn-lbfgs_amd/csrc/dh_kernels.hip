@@ -89,8 +89,11 @@ struct PriceArgs {
     int paired;             // option i under param set i, one option per task
     int strike_mode;
     int exact;              // validation mode (host routes to cos_exact_kernel)
-    int partials_only;      // loss requests of the device L-BFGS-B: every task stores its partial
-                            // and ends (no hand-off); the step kernel forms the sums
+    int partials_only;      // 1: loss requests of the device L-BFGS-B: every task stores its partial
+                            // (invalid flag in the sign bit) and ends (no hand-off); the step
+                            // kernel forms the sums.  2: multi-round fused requests: every task
+                            // stores its partial and invalid count and ends; loss_partials_kernel
+                            // then forms the sums as the hand-off's last task would
     int M;                  // options in the (sorted) option arrays
     int N;
     double L;
@@ -662,6 +665,10 @@ __device__ __forceinline__ int cf_cut_group8(const dh::Params& P, double T, doub
 // same values, so the same bits.
 // ----------------------------------------------------------------------------------------------
 constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane groups of a wave
+#ifndef DH_AHEAD_SKIP_STAGE
+#define DH_AHEAD_SKIP_STAGE 1
+#endif
+constexpr bool kAheadSkipStage = DH_AHEAD_SKIP_STAGE;   // the writer wave stages no options
 
 // v of lane (lane & ~7) | l: the 8-lane group's broadcast
 __device__ __forceinline__ double grp8_bcast(double v, int l) {
@@ -1226,6 +1233,13 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     const double f = nb;
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
+    if (A.partials_only == 2) {     // plain stores: loss_partials_kernel reads them next
+        if (t == 0) {
+            A.part_sse[task] = s;
+            A.part_bad[task] = (int)f;
+        }
+        return;
+    }
     if (A.partials_only) {          // plain stores: the next launch (the step kernel) reads them;
         // the tile's invalid flag rides in the sign bit (a valid partial is a sum of squares: +0,
         // positive, +inf or NaN, canonicalised to + here), so the step kernel reads one array
@@ -1254,6 +1268,29 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
         A.sse[p] = acc;
         A.n_bad[p] = (int)bad;
         __hip_atomic_store(&A.counter[p * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// The hand-off's last task, as its own launch after a partials_only == 2 request (one 64-lane
+// block per param set): the same reads in the same order and the same butterfly, so the same bits
+// as task_loss.  A multi-round fused grid's blocks then end with plain stores instead of the
+// agent-scope store drain and the ticket atomic (~1.8k cycles of every block's chain).
+__global__ __launch_bounds__(64) void loss_partials_kernel(const double* __restrict__ part_sse,
+                                                           const int* __restrict__ part_bad,
+                                                           int n_tiles, double* sse, int* n_bad) {
+    const int64_t p = blockIdx.x;
+    const int t = threadIdx.x;
+    const int64_t base_i = p * n_tiles;
+    double acc = 0.0, bad = 0.0;
+    for (int j = t; j < n_tiles; j += 64) {
+        acc += part_sse[base_i + j];
+        bad += part_bad[base_i + j];
+    }
+    acc = xor_sum(acc, 64);
+    bad = xor_sum(bad, 64);
+    if (t == 0) {
+        sse[p] = acc;
+        n_bad[p] = (int)bad;
     }
 }
 
@@ -2061,7 +2098,13 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const double* prm = H.prm + p * DH_PARAM_STRIDE;
     const double S0 = prm[13];
     dh::load_math_tables(sct, nthr > 64 ? 64 : 0);      // the waves after the prologue's
-    for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
+    // staging order: waves 1, 2, .., then 0 (its prologue first); a first-round block's writer
+    // wave stages nothing (its ahead_write chain is the longest before the barrier)
+    const bool ws = ahead_w && kAheadSkipStage;
+    int ts = (t + nthr - 64) % nthr;
+    if (ws && wv > wahead) ts -= 64;
+    if (ws && wv == 0) ts -= 64;
+    for (int i = ts; !(ws && wv == wahead) && i < gn; i += ws ? nthr - 64 : nthr) {
         const int m = g0 + i;
         const double K = option_strike(A, m, S0);
         double ratio;
@@ -2530,6 +2573,8 @@ struct dh_ctx {
     size_t ahead_flag_cap = 0;
     unsigned ahead_epoch = 0;
     int ahead_on = -1;
+    int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
+                               // in loss_partials_kernel (-1: not read yet)
     std::vector<std::pair<std::array<int64_t, 3>, int>> resident_fused;
 };
 
@@ -2746,6 +2791,12 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
             A.ahead_flag = (unsigned*)ctx->ahead_flag.ptr;
             A.ahead_stride = res;
             A.ahead_epoch = ctx->ahead_epoch;
+            // and the loss sums in a launch of their own (loss_partials_kernel)
+            if (ctx->defer_on < 0) {
+                const char* e = std::getenv("DHCOS_DEFER");
+                ctx->defer_on = (e && e[0] == '0') ? 0 : 1;
+            }
+            if (ctx->defer_on && A.part_sse && !A.partials_only && !A.paired) A.partials_only = 2;
         }
     }
     if (blocks >= kPrologueKernelMinBlocks && !ctx->stamps_on) {
@@ -2777,6 +2828,12 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         default: hipLaunchKernelGGL((cos_fused_kernel<256, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
     }
     HIP_TRY(hipGetLastError());
+    if (A.partials_only == 2) {
+        hipLaunchKernelGGL(loss_partials_kernel, dim3((unsigned)A.P), dim3(64), 0, st,
+                           (const double*)A.part_sse, (const int*)A.part_bad, A.n_tiles, A.sse,
+                           A.n_bad);
+        HIP_TRY(hipGetLastError());
+    }
     return DH_OK;
 }
 
