@@ -421,6 +421,40 @@ def test_calibrate_c2_single_start_matches_reference_algorithm(dh, driver):
     assert rel_close(res.final_loss, want["fun"], LOSS_RTOL, 0), (res.final_loss, want["fun"])
 
 
+@pytest.mark.parametrize("driver", ["scipy", "device"])
+def test_calibrate_c2_iterating_start_in_noise_ensemble(dh, driver):
+    """An iterating calibration at configs[1]'s scale (VERDICT r4 "missing" 3): calibrate(300, 1,
+    x0=start 1 of calibrate(300, 3) under np.random.seed(0)) on the bench's 1,024-option C2
+    surface at N = 256 (tests/golden/calib_c2_start1.json, make_calib_c2.py --start 1: the
+    reference algorithm -- oracle losses, SciPy's L-BFGS-B -- with member 0 noise-free and the
+    others at the GPU's measured price differences on this surface, 5.4e-13).  Asserted: the x0
+    (pinned to the reference's draws in test_oracle_golden.py), a message some member ends with,
+    the iteration count inside the members' range widened by a quarter of its width, and the loss
+    inside conftest.ensemble_band of the members' losses."""
+    import json
+    from conftest import GOLDEN, ensemble_band
+    with open(os.path.join(GOLDEN, "calib_c2_start1.json")) as fh:
+        g = json.load(fh)
+    mkt, S0, r, N = g["market"], g["S0"], g["r"], g["N"]
+    x0 = np.array(g["x0"])
+    np.random.seed(0)
+    assert np.array_equal(dh.DoubleHestonJumpCalibrator(S0, r, mkt, N=N).start_points(3)[1], x0)
+    res = dh.DoubleHestonJumpCalibrator(S0, r, mkt, N=N).calibrate(maxiter=300, multi_start=1,
+                                                                    x0=x0, driver=driver)
+    members = g["members"]
+    nits = [m["nit"] for m in members]
+    w = max(nits) - min(nits)
+    nit_lo, nit_hi = min(nits) - -(-w // 4), max(nits) + -(-w // 4)
+    lo, hi = ensemble_band([m["fun"] for m in members])
+    print(f"{driver}: nit {res.iterations} {res.message!r} loss {res.final_loss:.6e}; members: "
+          f"nit {min(nits)}..{max(nits)} loss {min(m['fun'] for m in members):.6e}.."
+          f"{max(m['fun'] for m in members):.6e} ({members[0]['message']!r})")
+    assert res.iterations > 0                           # it iterates (unlike start 0)
+    assert res.message in {m["message"] for m in members}, res.message
+    assert nit_lo <= res.iterations <= nit_hi, (res.iterations, nit_lo, nit_hi)
+    assert lo <= res.final_loss <= hi, (res.final_loss, lo, hi)
+
+
 def test_robust_start_matches_reference_exactly(dh, calib_golden):
     """Start 0 (literature guess on the Feller kink): ABNORMAL after 21 requests, nit 0 (Q12)."""
     from dhcos.calibrator import run_starts
