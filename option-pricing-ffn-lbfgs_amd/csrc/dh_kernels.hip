@@ -2268,8 +2268,11 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const Consts C{0.0 + red[0][0], 0.0 + red[1][0], 0.0 + red[2][0], 0.0 + red[3][0], a, b, eb, ea};
     if (t < tpt2) tile_sums_r<RT>(A, p, C, S0, disc, gn, G, tpt2, t, true, L, lclp + cap, sct);
     DH_STAMP(A, 4);
+    // (a block-wide tile reduced through LDS has just passed tile_sums' closing barrier, after
+    // its last loss terms were written: no second one)
+    const bool lds_red = tpt2 == kBlock && nthr == kBlock && (G > 64 || (G & (G - 1)) != 0);
     if (A.part_sse) {
-        __syncthreads();
+        if (!lds_red) __syncthreads();
         if (t < 64) {
             serial_prio(true);
             task_loss(A, p, A.paired ? p : p * A.n_tiles + g, gn, t, L.sse, L.bad);

@@ -35,7 +35,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from golden_common import ROOT, O, pinned_start_points  # noqa: E402
-from make_calib_noise import GEN_HI, GEN_LO, measured_eps, run_start  # noqa: E402
+from make_calib_noise import (GEN_HI, GEN_LO, HISTORY, N_MAX, measured_eps,  # noqa: E402
+                              member_eps, run_start)
 
 N = 256
 
@@ -53,7 +54,7 @@ def surface_c2():
 
 def _member(args):
     market, x0, m, S0, r, eps = args
-    e = 0.0 if m == 0 else eps
+    e = member_eps("c2", m, N_MAX["c2"]) if eps is None else (0.0 if m == 0 else eps)
     return dict(run_start(market, np.array(x0), e, 7000 + m, S0=S0, r=r, N=N, surface=True),
                 eps=e)
 
@@ -61,7 +62,7 @@ def _member(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--start", type=int, default=0, choices=[0, 1])
-    ap.add_argument("--members", type=int, default=8)
+    ap.add_argument("--members", type=int, default=24)
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--eps", type=float, default=None,
                     help="member noise scale (default: the measured C2 max, gpu_price_noise.json)")
@@ -72,8 +73,9 @@ def main():
     market, S0, r = surface_c2()
     x0 = pinned_start_points(DoubleHestonJumpCalibrator(S0, r, market, N=N), 3)[a.start].tolist()
     eps, eps_src = (a.eps, "--eps") if a.eps is not None else measured_eps("c2")
+    eps_r, src_r = measured_eps("c2", "rms")
     with mp.get_context("fork").Pool(a.procs) as pool:
-        members = pool.map(_member, [(market, x0, m, S0, r, eps) for m in range(a.members)])
+        members = pool.map(_member, [(market, x0, m, S0, r, a.eps) for m in range(a.members)])
     for m, mb in enumerate(members):
         print(m, mb, flush=True)
     funs = [mb["fun"] for mb in members]
@@ -81,8 +83,11 @@ def main():
     out = {"what": f"calibrate(300, 1) of the reference algorithm (oracle losses at N = 256, "
                    f"SciPy L-BFGS-B) on bench.py's C2 surface priced by the oracle, from start "
                    f"{a.start} of calibrate(300, 3) under np.random.seed(0); member 0 noise-free, "
-                   f"members 1.. prices x (1 + eps U(-1, 1)), eps = {eps:.3e} ({eps_src})",
-           "N": N, "market": market, "S0": S0, "r": r, "x0": x0, "start": a.start, "eps": eps,
+                   f"members 1.. prices x (1 + eps U(-1, 1)), eps = {eps:.3e} ({eps_src}) for "
+                   f"members 1 .. {N_MAX['c2'] - 1}"
+                   + ("" if a.eps is not None else f", {eps_r:.3e} ({src_r}) after"),
+           "history": HISTORY, "N": N, "market": market, "S0": S0, "r": r, "x0": x0,
+           "start": a.start, "eps": eps, "eps_rms": eps_r,
            "members": members, "fun_min": min(funs), "fun_max": max(funs),
            "nit_min": min(mb["nit"] for mb in members),
            "nit_max": max(mb["nit"] for mb in members)}

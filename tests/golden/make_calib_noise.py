@@ -69,14 +69,27 @@ def run_start(market, x0, eps, seed, scalar=False, S0=100.0, r=0.05, N=128, surf
             "message": str(res.message), "success": bool(res.success)}
 
 
-def measured_eps(name):
-    """The GPU's measured max relative price difference from the reference's pricer on surface
-    ``name`` (tests/golden/gpu_price_noise.json, measure_price_noise.py run on the GPU box) ->
-    (eps, where it came from)."""
+def measured_eps(name, kind="max"):
+    """The member noise scale from the GPU's measured relative price differences from the
+    reference's pricer on surface ``name`` (tests/golden/gpu_price_noise.json,
+    measure_price_noise.py run on the GPU box) -> (eps, where it came from).  kind "max": the
+    largest difference (U(-eps, eps) bounds every GPU difference); "rms": sqrt(3) x their RMS
+    (U(-eps, eps) has the GPU's RMS -- the max overstates the typical difference ~7-10x)."""
     path = os.path.join(ROOT, "tests", "golden", "gpu_price_noise.json")
     with open(path) as fh:
         g = json.load(fh)
+    if kind == "rms":
+        return float(np.sqrt(3.0) * g[name]["rms_rel"]), \
+            f"gpu_price_noise.json [{name}] sqrt(3) rms_rel"
     return float(g[name]["max_rel"]), f"gpu_price_noise.json [{name}] max_rel"
+
+
+def member_eps(name, m, n_max):
+    """Member m's noise scale: 0 for member 0 (noise-free), the measured max for members
+    1 .. n_max - 1, the RMS-matched scale for the rest (measured_eps)."""
+    if m == 0:
+        return 0.0
+    return measured_eps(name, "max" if m < n_max else "rms")[0]
 
 
 GEN_LO = np.array([0.025, 1.5, 0.025, 0.2, -0.85, 0.02, 0.3, 0.025, 0.1, -0.7, 0.05, -0.08, 0.03])
@@ -96,10 +109,10 @@ def surface_5x5():
 
 
 def _member(args):
-    market, x0s, m, S0, r, eps_m = args
+    market, x0s, m, S0, r, name, n_max = args
     # member 0: the reference-exact scalar pricer, noise-free; the others: the GPU's measured
-    # price differences on this surface as noise
-    eps = 0.0 if m == 0 else eps_m
+    # price differences on this surface as noise (member_eps)
+    eps = member_eps(name, m, n_max)
     starts = [run_start(market, np.array(x0), eps, 1000 * m + s, scalar=(m == 0), S0=S0, r=r)
               for s, x0 in enumerate(x0s)]
     best, best_loss = None, np.inf
@@ -113,9 +126,13 @@ def _member(args):
 
 HISTORY = ("round 4: members at 1e-15 only; the GPU's start 2 on the 5 x 5 surface then ended "
            "CONVERGENCE where all of them ended ABNORMAL (gpurun_out/t_mt.log), and 12 members at "
-           "1e-13 were added after that run.  Round 5: every member at the GPU's measured max "
-           "relative price difference from the reference's pricer on the surface "
-           "(gpu_price_noise.json, measure_price_noise.py), no scale chosen after a GPU result")
+           "1e-13 were added after that run.  Round 5: members at the GPU's measured relative "
+           "price differences from the reference's pricer on the surface (gpu_price_noise.json, "
+           "measure_price_noise.py): the max (members 1 .. n_max - 1) and, added after the C2 "
+           "iterating-start fixture's 8 max-scale members all ended ABNORMAL where the GPU "
+           "converged, sqrt(3) x the RMS (the scale whose uniform noise has the GPU's RMS; the max "
+           "overstates the typical difference 7-10x), for every ensemble alike")
+N_MAX = {"test_market": 12, "5x5": 16, "c2": 8}     # members 1 .. N_MAX - 1 at the max scale
 
 
 def main_surface(members_n, procs):
@@ -127,8 +144,10 @@ def main_surface(members_n, procs):
     market, S0, r = surface_5x5()
     x0s = [x.tolist() for x in pinned_start_points(DoubleHestonJumpCalibrator(S0, r, market), 3)]
     eps, src = measured_eps("5x5")
+    eps_r, src_r = measured_eps("5x5", "rms")
     with mp.get_context("fork").Pool(procs) as pool:
-        members = pool.map(_member, [(market, x0s, m, S0, r, eps) for m in range(members_n)])
+        members = pool.map(_member, [(market, x0s, m, S0, r, "5x5", N_MAX["5x5"])
+                                     for m in range(members_n)])
     for m, mb in enumerate(members):
         print(m, mb["best_start"], mb["final_loss"], mb["iterations"], mb["message"],
               [(s["nit"], s["message"][:12], round(s["fun"], 12)) for s in mb["starts"]])
@@ -136,8 +155,9 @@ def main_surface(members_n, procs):
     out = {"what": "calibrate(300, 3) of the reference algorithm (oracle losses at N = 128, SciPy "
                    "L-BFGS-B) on a 5 x 5 synthetic surface (make_calib_noise.py surface_5x5), "
                    f"np.random.seed(0) starts, prices x (1 + eps U(-1, 1)) per member, eps = "
-                   f"{eps:.3e} ({src}); member 0: the reference-exact scalar pricer, noise-free",
-           "history": HISTORY, "eps": eps,
+                   f"{eps:.3e} ({src}) for members 1 .. {N_MAX['5x5'] - 1}, {eps_r:.3e} "
+                   f"({src_r}) after; member 0: the reference-exact scalar pricer, noise-free",
+           "history": HISTORY, "eps": eps, "eps_rms": eps_r,
            "market": market, "S0": S0, "r": r, "x0s": x0s,
            "members": members, "final_loss_min": min(winners), "final_loss_max": max(winners)}
     with open(os.path.join(ROOT, "tests", "golden", "calib_noise_5x5.json"), "w") as fh:
@@ -146,7 +166,7 @@ def main_surface(members_n, procs):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--members", type=int, default=12)
+    ap.add_argument("--members", type=int, default=24)
     ap.add_argument("--surface", default=None, choices=[None, "5x5"])
     ap.add_argument("--procs", type=int, default=6)
     a = ap.parse_args()
@@ -157,10 +177,11 @@ def main():
     market = g["test_market"]
     x0s = [s["x0"] for s in g["calibrate_seed0_starts"]]
     eps, src = measured_eps("test_market")
+    eps_r, src_r = measured_eps("test_market", "rms")
     import multiprocessing as mp
     with mp.get_context("fork").Pool(a.procs) as pool:
-        members = pool.map(_member, [(market, x0s, m, 100.0, 0.05, eps)
-                                     for m in range(a.members)])
+        members = pool.map(_member, [(market, x0s, m, 100.0, 0.05, "test_market",
+                                      N_MAX["test_market"]) for m in range(a.members)])
     for m, mb in enumerate(members):
         print(m, mb["best_start"], mb["final_loss"], mb["iterations"], mb["message"],
               [(s["nit"], round(s["fun"], 12)) for s in mb["starts"]], flush=True)
@@ -168,10 +189,10 @@ def main():
     out = {"what": "calibrate(300, 3) of the reference algorithm (oracle losses, SciPy L-BFGS-B) "
                    "on tests/test_suite.py's market, np.random.seed(0) starts (the reference's own "
                    f"draws, calib.json), prices x (1 + eps U(-1, 1)) per member, eps = {eps:.3e} "
-                   f"({src}); member 0: the reference-exact scalar pricer, noise-free",
-           "history": "round 3-4: members at 1e-15.  Round 5: every member at the GPU's measured "
-                      "max relative price difference on this market (gpu_price_noise.json)",
-           "eps": eps,
+                   f"({src}) for members 1 .. {N_MAX['test_market'] - 1}, {eps_r:.3e} ({src_r}) "
+                   f"after; member 0: the reference-exact scalar pricer, noise-free",
+           "history": "round 3-4: members at 1e-15.  " + HISTORY[HISTORY.index("Round 5"):],
+           "eps": eps, "eps_rms": eps_r,
            "members": members, "final_loss_min": min(winners), "final_loss_max": max(winners)}
     with open(os.path.join(ROOT, "tests", "golden", "calib_noise.json"), "w") as fh:
         json.dump(out, fh, indent=1)

@@ -23,7 +23,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel",
+KERNELS = ("loss_partials_kernel", "cos_fused_kernel", "cos_table_kernel", "cos_option_small_kernel", "cos_option_kernel",
            "table_prologue_kernel", "cos_gen_kernel")
 
 
@@ -83,9 +83,13 @@ def main():
         elif total.get("cos_fused_kernel", 0.0) >= max(total.values()):
             # large fused grids run table_prologue_kernel ahead of the fused kernel
             pro = total.get("table_prologue_kernel", 0.0) >= 0.01 * total["cos_fused_kernel"]
-            req_kernels = (("table_prologue_kernel",) if pro else ()) + ("cos_fused_kernel",)
+            # multi-round loss requests sum their tiles' partials in a launch of their own
+            fin = total.get("loss_partials_kernel", 0.0) >= 0.001 * total["cos_fused_kernel"]
+            req_kernels = ((("table_prologue_kernel",) if pro else ()) + ("cos_fused_kernel",)
+                           + (("loss_partials_kernel",) if fin else ()))
         else:
-            opt = max((k for k in KERNELS[2:4] if k in total), key=lambda k: total[k])
+            opt = max((k for k in ("cos_option_small_kernel", "cos_option_kernel") if k in total),
+                      key=lambda k: total[k])
             req_kernels = ("cos_table_kernel", opt)
         vals = collections.defaultdict(list)
         for f in glob.glob(os.path.join(args.src, f"{args.tag}_{c}_pmc*_counter_collection.csv")):
