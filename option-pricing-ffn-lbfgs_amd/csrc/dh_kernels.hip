@@ -666,7 +666,7 @@ __device__ __forceinline__ int cf_cut_group8(const dh::Params& P, double T, doub
 // ----------------------------------------------------------------------------------------------
 constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane groups of a wave
 #ifndef DH_AHEAD_SKIP_STAGE
-#define DH_AHEAD_SKIP_STAGE 1
+#define DH_AHEAD_SKIP_STAGE 0     // 1 measured slower on C3 (58.5 vs 57.8 us kernel)
 #endif
 constexpr bool kAheadSkipStage = DH_AHEAD_SKIP_STAGE;   // the writer wave stages no options
 
@@ -2269,8 +2269,13 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     if (t < tpt2) tile_sums_r<RT>(A, p, C, S0, disc, gn, G, tpt2, t, true, L, lclp + cap, sct);
     DH_STAMP(A, 4);
     // (a block-wide tile reduced through LDS has just passed tile_sums' closing barrier, after
-    // its last loss terms were written: no second one)
-    const bool lds_red = tpt2 == kBlock && nthr == kBlock && (G > 64 || (G & (G - 1)) != 0);
+    // its last loss terms were written, so a second one is not needed; measured, dropping it was
+    // slower on C3: 57.8 vs 57.45 us per request)
+#ifndef DH_SKIP_HANDOFF_BARRIER
+#define DH_SKIP_HANDOFF_BARRIER 0
+#endif
+    const bool lds_red = DH_SKIP_HANDOFF_BARRIER && tpt2 == kBlock && nthr == kBlock &&
+                         (G > 64 || (G & (G - 1)) != 0);
     if (A.part_sse) {
         if (!lds_red) __syncthreads();
         if (t < 64) {

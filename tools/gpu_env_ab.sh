@@ -8,7 +8,7 @@ CONFIG=${CONFIG:-c3}
 for rep in $(seq 1 ${REPS:-2}); do
   for v in ${VARIANTS:-base}; do
     envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
-    out=gpurun_out/ab/${CONFIG}_$(echo "$v" | tr '=,' '__')_$rep
+    out=gpurun_out/ab/${CONFIG}_$(echo "$v" | tr '=,/.' '____')_$rep
     timeout -k 10 150 env $envs python3 bench.py --config $CONFIG --no-cpu --no-calib --no-side \
         --steps ${STEPS:-200} --warmup 20 > $out.json 2> $out.err || { echo "$v failed"; tail -3 $out.err; exit 1; }
     python3 -c "
