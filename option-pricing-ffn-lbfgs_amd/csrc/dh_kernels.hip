@@ -665,6 +665,12 @@ __device__ __forceinline__ int cf_cut_group8(const dh::Params& P, double T, doub
 // same values, so the same bits.
 // ----------------------------------------------------------------------------------------------
 constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane groups of a wave
+// What travels per later table: the prologue's values that cost a transcendental or a cumulant
+// chain -- a, b, e^b, e^a, the clamp bounds' slots 25 and 26, e^{-rT}, the CF drift and K_cf --
+// at ahead[q * kAheadRec + i] (one 128-byte line per table, the writer group's 8 lanes storing 8
+// of them in one coalesced store); the reader re-forms the other slots (2/(b - a), pi/(b - a), the
+// factors' constants, S0, r, T, the group) from the parameters by the same expressions.
+constexpr int kAheadRec = 16;
 #ifndef DH_AHEAD_SKIP_STAGE
 #define DH_AHEAD_SKIP_STAGE 0     // 1 measured slower on C3 (58.5 vs 57.8 us kernel)
 #endif
@@ -683,6 +689,10 @@ __device__ __forceinline__ void agent_store(double* p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ double agent_load(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The later table of 8-lane group lane / 8 of first-round block q0: q0 + (j + 1) R (act: it
 // exists; an inactive group runs in step on q0's own table and stores nothing)
 __device__ __forceinline__ int64_t ahead_table(const PriceArgs& A, int64_t q0, int64_t nblocks,
@@ -693,8 +703,8 @@ __device__ __forceinline__ int64_t ahead_table(const PriceArgs& A, int64_t q0, i
 }
 
 // The writer (the staging wave, before the first barrier): tables q0 + (j + 1) R, j = lane / 8,
-// slots 0 .. 29 into ahead[]; each group's truncation range into ab[j] for the cut wave, which
-// forms slot 30 (K_cf) during the CF loop (ahead_cut)
+// values 0 .. 7 of the record into ahead[]; each group's truncation range into ab[j] for the cut
+// wave, which forms value 8 (K_cf) during the CF loop (ahead_cut)
 __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead& H, int64_t q0,
                                             int64_t nblocks, int lane, double (*ab)[2]) {
 #pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
@@ -717,8 +727,6 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
     const double h = A.L * sqrt(fabs(c2));
     const double a = c1 - h;                       // trunc_unclamped (double_heston.py:120-132)
     const double b = c1 + h;
-    int2 gr = make_int2((int)p, 1);
-    if (!H.paired) gr = H.groups[g];
     const dh::FactorC Fj = dh::factor_consts(v0, k, th, sg, rh);
     const int e_lane = sub < 6 ? sub : 0;
     const double arg = e_lane == 0 ? b : e_lane == 1 ? a : e_lane == 2 ? a + 0.1
@@ -738,30 +746,65 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
     CC.half_sj2 = 0.5 * (P.sj * P.sj);
     CC.muj = P.muj;
     CC.lt = P.lam * T;
-    const double e0 = grp8_bcast(e, 0), e1 = grp8_bcast(e, 1), e2 = grp8_bcast(e, 2);
-    const double e3 = grp8_bcast(e, 3), e5 = grp8_bcast(e, 5);
     if (sub == 0) {
         ab[lane >> 3][0] = a;
         ab[lane >> 3][1] = b;
     }
-    if (act && sub == 0) {
-        double* c = A.ahead + qa * kTabC;
-        agent_store(c + 0, a);
-        agent_store(c + 1, b);
-        agent_store(c + 2, e0);
-        agent_store(c + 3, e1);
-        agent_store(c + 4, 2.0 / (b - a));
-        agent_store(c + 5, dh::kPi / (b - a));
-        const double* cc = (const double*)&CC;
-        for (int i = 0; i < 16; ++i) agent_store(c + 6 + i, cc[i]);
-        agent_store(c + 22, P.S0);
-        agent_store(c + 23, P.r);
-        agent_store(c + 24, T);
-        agent_store(c + 25, e2 * (1.0 + kClampMargin));
-        agent_store(c + 26, e3 * (1.0 - kClampMargin));
-        agent_store(c + 27, gr.x);
-        agent_store(c + 28, gr.y);
-        agent_store(c + 29, e5);
+    // record value sub of the group's table: a, b, e^b, e^a, slot 25, slot 26, e^{-rT}, drift
+    const double e2 = grp8_bcast(e, 2), e3 = grp8_bcast(e, 3);
+    double v = sub == 0 ? a : sub == 1 ? b : grp8_bcast(e, sub == 2 ? 0 : sub == 3 ? 1 : 5);
+    v = sub == 4 ? e2 * (1.0 + kClampMargin) : v;
+    v = sub == 5 ? e3 * (1.0 - kClampMargin) : v;
+    v = sub == 7 ? CC.drift : v;
+    if (act) agent_store(A.ahead + qa * kAheadRec + sub, v);
+}
+
+// The reader (wave 0 of a later block whose flag is set): the record's values and the slots
+// re-formed from the parameters, into c[0 .. 30) -- table_prologue_wave's expressions on the
+// same operands, uncontracted, so the same bits
+__device__ __forceinline__ void ahead_read(const PriceArgs& A, const FusedHead& H, int64_t q,
+                                           double* c, int lane) {
+#pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
+    const double v = agent_load(A.ahead + q * kAheadRec + (lane < 8 ? lane : 0));
+    const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
+    const int g = (int)((unsigned)q % (unsigned)H.tpp);
+    const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
+    const double T = H.tsrc[H.paired ? p : g];
+    int2 gr = make_int2((int)p, 1);
+    if (!H.paired) gr = H.groups[g];
+    const double a = lane_bcast(v, 0), b = lane_bcast(v, 1);
+    const bool two = lane & 1;                     // factor 2 on odd lanes (table_prologue_wave)
+    const dh::FactorC Fj = two ? dh::factor_consts(P.v02, P.k2, P.t2, P.s2, P.r2)
+                               : dh::factor_consts(P.v01, P.k1, P.t1, P.s1, P.r1);
+    const double* fj = (const double*)&Fj;
+    double f1[6], f2[6];
+    for (int i = 0; i < 6; ++i) {
+        f1[i] = lane_bcast(fj[i], 0);
+        f2[i] = lane_bcast(fj[i], 1);
+    }
+    if (lane == 0) {
+        c[0] = a;
+        c[1] = b;
+        c[2] = lane_bcast(v, 2);
+        c[3] = lane_bcast(v, 3);
+        c[4] = 2.0 / (b - a);
+        c[5] = dh::kPi / (b - a);
+        for (int i = 0; i < 6; ++i) {
+            c[6 + i] = f1[i];
+            c[12 + i] = f2[i];
+        }
+        c[18] = lane_bcast(v, 7);                  // drift
+        c[19] = 0.5 * (P.sj * P.sj);               // half_sj2
+        c[20] = P.muj;
+        c[21] = P.lam * T;                         // lt
+        c[22] = P.S0;
+        c[23] = P.r;
+        c[24] = T;
+        c[25] = lane_bcast(v, 4);
+        c[26] = lane_bcast(v, 5);
+        c[27] = gr.x;
+        c[28] = gr.y;
+        c[29] = lane_bcast(v, 6);
     }
 }
 
@@ -781,7 +824,7 @@ __device__ __forceinline__ void ahead_cut(const PriceArgs& A, const FusedHead& H
                         ? A.N
                         : cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N,
                                         lane & 7);
-    if (act && (lane & 7) == 0) agent_store(A.ahead + q * kTabC + 30, kcf);
+    if (act && (lane & 7) == 0) agent_store(A.ahead + q * kAheadRec + 8, kcf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -802,9 +845,6 @@ __device__ __forceinline__ bool ahead_ready(const PriceArgs& A, int64_t q) {
     return __builtin_amdgcn_readfirstlane(f) == A.ahead_epoch;
 }
 
-__device__ __forceinline__ double agent_load(const double* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Every table's prologue of a large fused request ahead of the fused launch (launch_fused): the
 // fused blocks then load their constants instead of running the one-wave prologue chain while
@@ -2069,13 +2109,14 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         // (each of the two waves decides on its own flag load and fills its own slots: loaded or
         // formed, the same values, so a flag set between the two loads changes nothing)
         if (ahead_r && ahead_ready(A, q)) {
-            if (lane < (wcut == 0 ? kTabC : 30)) shc[lane] = agent_load(A.ahead + q * kTabC + lane);
+            ahead_read(A, H, q, shc, lane);
+            if (wcut == 0 && lane == 0) shc[30] = agent_load(A.ahead + q * kAheadRec + 8);
         } else {
             table_prologue_wave(A, H, q, shc, lane, wcut == 0);
         }
     } else if (wv == wcut) {
         if (ahead_r && ahead_ready(A, q)) {
-            if (lane == 0) shc[30] = agent_load(A.ahead + q * kTabC + 30);
+            if (lane == 0) shc[30] = agent_load(A.ahead + q * kAheadRec + 8);
         } else {
             const int kcf = A.N < kCfCutMinN ? A.N : prologue_cut_wave(A, H, q, lane);
             if (lane == 0) shc[30] = kcf;
@@ -2788,7 +2829,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
             ctx->resident_fused.push_back({key, res});
         }
         if (blocks > res) {
-            HIP_TRY(ctx->ahead.reserve((size_t)blocks * kTabC * sizeof(double)));
+            HIP_TRY(ctx->ahead.reserve((size_t)blocks * kAheadRec * sizeof(double)));
             if ((size_t)blocks > ctx->ahead_flag_cap) {
                 HIP_TRY(ctx->ahead_flag.reserve((size_t)blocks * sizeof(unsigned)));
                 HIP_TRY(hipMemsetAsync(ctx->ahead_flag.ptr, 0, ctx->ahead_flag.cap, st));
