@@ -555,6 +555,26 @@ class FgChannel:
                        C.c_void_p(self._g.ctypes.data), C.c_void_p(self._low.ctypes.data))
         self._lock = surf.ctx._lock
         self._fg_s = surf.ctx._fg_s
+        self._consts = (float(S0), float(r), int(N), float(L))
+
+    def loop_slot(self):
+        """The slot's buffers as the native request loop takes them (dhcos._scipy_loop.run):
+        x, model, f, g, low, and per request size S the packed exp / tanh columns."""
+        ev = [None] + [np.empty(2 * S * 10) for S in range(1, self.s_max + 1)]
+        tv = [None] + [np.empty(2 * S * 2) for S in range(1, self.s_max + 1)]
+        return (self._x, self._m, self._f, self._g, self._low, ev, tv)
+
+    def loop_device(self):
+        """The C-ABI entry points and handles the native request loop calls
+        (dh_surface_fg_begin / _end / _cancel on this channel's surface and constants)."""
+        lib = load()
+
+        def addr(name):
+            return C.cast(lib[name], C.c_void_p).value
+        S0, r, N, L = self._consts
+        return (addr("dh_surface_fg_begin"), addr("dh_surface_fg_end"),
+                addr("dh_surface_fg_cancel"), self.surf.ctx.handle.value, self.surf.handle.value,
+                S0, r, N, L)
 
     def model_out(self, S: int) -> np.ndarray:
         """The [2, S, 13] model buffer of a request of S starts (fd_models(..., out=))."""

@@ -570,10 +570,23 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
     order = [list(range(n))] if lockstep else [[s] for s in range(n)]
     surf = _pipeline_surface(cal, n, pipeline) if (lockstep and pipeline is not False) else None
     with _single_threaded_blas():
+        loop = _scipy_loop()
         if surf is not None:
-            _advance_pipelined(cal, surf, gens, states, outcomes)
+            if loop is not None:
+                _run_native(loop, cal, surf, x0s, [list(range(0, n, 2)), list(range(1, n, 2))],
+                            maxiter, states, outcomes)
+            else:
+                _advance_pipelined(cal, surf, gens, states, outcomes)
         else:
-            _advance(cal, gens, states, order, outcomes)
+            nsurf = _native_surface(cal, max(len(g) for g in order)) if loop else None
+            if nsurf is not None:
+                launches = 0
+                for group in order:
+                    _run_native(loop, cal, nsurf, x0s, [group], maxiter, states, outcomes)
+                    launches += cal.lockstep_launches
+                cal.lockstep_launches = launches
+            else:
+                _advance(cal, gens, states, order, outcomes)
     cal.start_stats = [(st.n_calls, st.best_loss) for st in states]
     last = states[-1]
     cal.n_calls, cal.best_loss = last.n_calls, last.best_loss   # state after the last start
@@ -768,6 +781,91 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
                 except Exception:      # noqa: BLE001 -- unwinding: the first error wins
                     pass
     cal.lockstep_launches = launches
+
+
+_LOOP = None
+
+
+def _scipy_loop():
+    """The native request loop (dhcos._scipy_loop, csrc/dh_scipy_loop.cpp), or None where the
+    Python loop runs: $DHCOS_NATIVE_LOOP = 0, or NumPy's error state set to raise / call on a
+    floating-point error (fd_models may then raise for one start, which the Python loop drops
+    alone).  The module is part of the build (make -C option-pricing-ffn-lbfgs_amd/csrc): a
+    missing one is an error, not a silent fallback."""
+    global _LOOP
+    if os.environ.get("DHCOS_NATIVE_LOOP", "") == "0":
+        return None
+    if any(v in ("raise", "call") for v in np.geterr().values()):
+        return None
+    if _LOOP is None:
+        try:
+            from . import _scipy_loop as mod
+        except ImportError as exc:
+            raise _native.NativeError(
+                "dhcos/_scipy_loop is not built; run `make -C option-pricing-ffn-lbfgs_amd/csrc` "
+                "(or set DHCOS_NATIVE_LOOP=0 for the Python loop)") from exc
+        _LOOP = mod
+    return _LOOP
+
+
+_LBFGSB_M = 10
+
+
+def _lbfgsb_arrays(x0):
+    """One start's setulb arrays as lbfgsb_steps allocates them (x = x0, no bounds), plus the
+    float64 g the loop hands to setulb."""
+    n, m = N_PARAMS, _LBFGSB_M
+    return (np.array(np.asarray(x0).ravel(), dtype=np.float64), np.zeros(n, np.float64),
+            np.zeros(n, np.float64), np.zeros(n, np.int32),
+            np.zeros(2 * m * n + 5 * n + 11 * m * m + 8 * m, np.float64),
+            np.zeros(3 * n, dtype=np.int32), np.zeros(2, dtype=np.int32),
+            np.zeros(4, dtype=np.int32), np.zeros(44, dtype=np.int32), np.zeros(29, np.float64),
+            np.zeros(2, dtype=np.int32), np.zeros(n, np.float64))
+
+
+def _loop_consts(maxiter):
+    return (_LBFGSB_M, 1e-9 / np.finfo(float).eps, 1e-6, 20, int(maxiter), _MAXFUN,
+            FD_ABS_STEP, _SQRT_EPS)
+
+
+def _loop_results(rows, arrs, maxiter, states, outcomes, ids):
+    """The native loop's per-start rows -> _StartState counters and lbfgsb_steps' OptimizeResult
+    (the same fields and message) for the starts in ids that finished."""
+    for s in ids:
+        state, f, g, nfev, nit, t_done, n_calls, best = rows[s]
+        states[s].n_calls, states[s].best_loss = n_calls, best
+        if state != 0:
+            continue                                   # dropped: setulb raised (except -> continue)
+        task = arrs[s][6]
+        if task[0] == 4:
+            warnflag = 0
+        elif nfev > _MAXFUN or nit >= maxiter:
+            warnflag = 1
+        else:
+            warnflag = 2
+        msg = status_messages[task[0]] + ": " + task_messages[task[1]]
+        res = OptimizeResult(fun=np.float64(f), jac=np.array(g), nfev=nfev, njev=nfev, nit=nit,
+                             status=warnflag, message=msg, x=arrs[s][0], success=(warnflag == 0))
+        outcomes[s] = (res, t_done)
+
+
+def _run_native(loop, cal, surf, x0s, groups, maxiter, states, outcomes):
+    """run_starts' request loop in native code (csrc/dh_scipy_loop.cpp): _advance_pipelined with
+    two groups, _advance's lockstep loop with one; the same setulb calls, fd_models bits and
+    per-start bookkeeping (tests/test_scipy_loop.py; tests/test_gpu_parity.py holds the two
+    loops' calibrations equal bit for bit).  The context's request slots are held for the call."""
+    arrs = [_lbfgsb_arrays(x0) for x0 in x0s]
+    chans = [_native.FgChannel(surf, k, max(1, len(g)), cal.spot, cal.risk_free_rate, cal.N)
+             for k, g in enumerate(groups)]
+    with surf.ctx._lock:
+        rc, launches, evals, rows = loop.run(chans[0].loop_device(), [list(g) for g in groups],
+                                             [ch.loop_slot() for ch in chans], arrs,
+                                             _lbfgsb.setulb, np.exp, np.tanh,
+                                             _loop_consts(maxiter))
+    cal.loss_evals += evals
+    cal.lockstep_launches = launches
+    _native._check(rc)
+    _loop_results(rows, arrs, maxiter, states, outcomes, [s for g in groups for s in g])
 
 
 def run_starts_device(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int):

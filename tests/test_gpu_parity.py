@@ -492,6 +492,33 @@ def test_lockstep_equals_sequential(dh, calib_golden):
     assert p_launches == max(nfev[0::2]) + max(nfev[1::2])   # one per group round
 
 
+@pytest.mark.parametrize("mode", ["pipelined", "lockstep", "sequential"])
+def test_native_loop_equals_python_loop(dh, calib_golden, monkeypatch, mode):
+    """The SciPy driver's native request loop (csrc/dh_scipy_loop.cpp, dhcos._scipy_loop) and the
+    Python loop it replaces ($DHCOS_NATIVE_LOOP=0: lbfgsb_steps generators, fd_models, FgChannel)
+    give the same calibration bit for bit -- x, fun, jac, nit, nfev, message, the per-start
+    n_calls / best loss and the launch count -- for the three seed-0 starts of the reference's
+    test market, in each of run_starts' three orders."""
+    from dhcos import calibrator as CM
+    g = calib_golden
+    x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
+    kw = {"pipelined": dict(lockstep=True, pipeline=True),
+          "lockstep": dict(lockstep=True, pipeline=False),
+          "sequential": dict(lockstep=False)}[mode]
+    outs = {}
+    for native in ("1", "0"):
+        monkeypatch.setenv("DHCOS_NATIVE_LOOP", native)
+        assert (CM._scipy_loop() is not None) == (native == "1")
+        cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+        runs = CM.run_starts(cal, x0s, 300, **kw)
+        outs[native] = (runs, cal.start_stats, cal.lockstep_launches, cal.loss_evals)
+    (a, sa, la, ea), (b, sb, lb, eb) = outs["1"], outs["0"]
+    for (ra, _), (rb, _) in zip(a, b):
+        assert np.array_equal(ra.x, rb.x) and ra.fun == rb.fun and np.array_equal(ra.jac, rb.jac)
+        assert (ra.nit, ra.nfev, ra.message, ra.status) == (rb.nit, rb.nfev, rb.message, rb.status)
+    assert sa == sb and (la, ea) == (lb, eb)
+
+
 def test_fg_begin_end_slots(dh, calib_golden):
     """The asynchronous halves of dh_surface_fg: two requests in flight (one per slot) give
     fg's bits; a busy slot, an empty slot and a bad slot index are errors."""
