@@ -755,9 +755,12 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
         ab[lane >> 3][0] = a;
         ab[lane >> 3][1] = b;
     }
-    // record value sub of the group's table: a, b, e^b, e^a, slot 25, slot 26, e^{-rT}, drift
+    // record value sub of the group's table: a, b, e^b, e^a, slot 25, slot 26, e^{-rT}, drift.
+    // The shuffles run on every lane, outside the selection: a lane shuffle inside a branch would
+    // read the branch's inactive lanes (sub-lanes 0 and 1 hold e^b and e^a)
     const double e2 = grp8_bcast(e, 2), e3 = grp8_bcast(e, 3);
-    double v = sub == 0 ? a : sub == 1 ? b : grp8_bcast(e, sub == 2 ? 0 : sub == 3 ? 1 : 5);
+    const double es = grp8_bcast(e, sub == 2 ? 0 : sub == 3 ? 1 : 5);
+    double v = sub == 0 ? a : sub == 1 ? b : es;
     v = sub == 4 ? e2 * (1.0 + kClampMargin) : v;
     v = sub == 5 ? e3 * (1.0 - kClampMargin) : v;
     v = sub == 7 ? CC.drift : v;
