@@ -151,11 +151,13 @@ int dh_surface_loss_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params
 int dh_surface_fg(dh_ctx* ctx, const dh_surface* s, const double* x0, const double* model, int S,
                   double S0, double r, int N, double L, double* f, double* g, double* low);
 /* The same request in two halves, so a host driver can run one group of starts' optimizer steps
- * while another group's request is on the device: begin forms the records into slot (0 or 1; each
- * slot owns its pinned buffers) and enqueues the request on the context's stream, then returns;
+ * while other groups' requests are on the device: begin forms the records into slot (0 ..
+ * DH_FG_SLOTS - 1; each slot owns its pinned buffers) and enqueues the request on the context's
+ * stream, then returns;
  * end waits for that slot's request and writes f, g, low as dh_surface_fg would (the same bits:
  * a start's values depend only on its own x0).  A slot holds one request at a time; requests
  * run in enqueue order; 14 S <= 1024 (larger: dh_surface_fg).                                   */
+#define DH_FG_SLOTS 4
 int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const double* x0, const double* model,
                         int S, double S0, double r, int N, double L, int slot);
 /* end: S must be the start count the slot's request was enqueued with, and s its surface

@@ -2626,7 +2626,7 @@ struct dh_ctx {
         HostBuf h_flag;
         unsigned flag_epoch = 0;
         bool flag_armed = false;
-    } fg[2];
+    } fg[DH_FG_SLOTS];
     // the flags the next loss launch posts (set by dh_surface_fg_begin around its launch) and
     // $DHCOS_FG_FLAG (-1: not read yet; 0: completion by events instead)
     unsigned* fg_done_arm = nullptr;
@@ -4539,7 +4539,7 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
                                    const double* model, int S, double S0, double r, int N,
                                    double L, int slot) {
     if (!ctx || !s || (S > 0 && !x0)) return fail(DH_E_ARG, "null argument");
-    if (slot < 0 || slot > 1) return fail(DH_E_ARG, "slot must be 0 or 1");
+    if (slot < 0 || slot >= DH_FG_SLOTS) return fail(DH_E_ARG, "slot out of range");
     int rc = fg_check(ctx, s, S);
     if (rc) return rc;
     rc = check_N(N);
@@ -4555,13 +4555,14 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     // buffer, table / clamp workspaces), whose sizes follow from the surface, N and the param-set
     // count only.  A grow frees buffers the other slot's enqueued launch still reads.  hipFree
     // happens to synchronise the device first, but nothing here relies on that: wait for the
-    // other slot whenever this request is not covered by an earlier one on the same surface and
-    // N (the pipelined SciPy driver's requests always are, after its first two).
-    auto& O = ctx->fg[1 - slot];
+    // other slots (their requests share the stream) whenever this request is not covered by an
+    // earlier one on the same surface and N (the pipelined SciPy driver's requests always are,
+    // after its first round).
     const size_t units = P * (size_t)std::max(s->n_tiles, s->n_groups);
     const bool covered = s == ctx->fg_surf && N == ctx->fg_N && units <= ctx->fg_max_units;
-    if (O.pending && !covered)
-        HIP_TRY(O.flag_armed ? hipStreamSynchronize(ctx->stream) : hipEventSynchronize(O.done));
+    bool others = false;
+    for (int o = 0; o < DH_FG_SLOTS; ++o) others = others || (o != slot && ctx->fg[o].pending);
+    if (others && !covered) HIP_TRY(hipStreamSynchronize(ctx->stream));
     if (s != ctx->fg_surf || N != ctx->fg_N) {
         ctx->fg_surf = s;
         ctx->fg_N = N;
@@ -4614,7 +4615,7 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
 extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, int S, double* f,
                                  double* g, double* low) {
     if (!ctx || !s) return fail(DH_E_ARG, "null argument");
-    if (slot < 0 || slot > 1) return fail(DH_E_ARG, "slot must be 0 or 1");
+    if (slot < 0 || slot >= DH_FG_SLOTS) return fail(DH_E_ARG, "slot out of range");
     auto& F = ctx->fg[slot];
     if (!F.pending) return fail(DH_E_ARG, "no request in flight in this slot");
     // the slot belongs to the context: the caller must name the request it enqueued (its surface
@@ -4665,7 +4666,7 @@ extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, int
 
 extern "C" int dh_surface_fg_cancel(dh_ctx* ctx, int slot) {
     if (!ctx) return fail(DH_E_ARG, "null argument");
-    if (slot < 0 || slot > 1) return fail(DH_E_ARG, "slot must be 0 or 1");
+    if (slot < 0 || slot >= DH_FG_SLOTS) return fail(DH_E_ARG, "slot out of range");
     auto& F = ctx->fg[slot];
     if (!F.pending) return DH_OK;
     DeviceScope dev_scope(ctx->device);

@@ -12,7 +12,7 @@
 //     columns (the same inner loops as fd_models, so the same bits: tests/test_scipy_loop.py);
 //   - the loop around setulb restates lbfgsb_steps (scipy/optimize/_lbfgsb_py.py, SciPy 1.15.3:
 //     ScalarFunction's re-evaluation test, the maxiter / maxfun stops) and _advance_pipelined /
-//     _consume (two groups of starts on two request slots, per-start n_calls and best loss).
+//     _consume (groups of starts on their own request slots, per-start n_calls and best loss).
 // The device calls are libdhcos's C-ABI through addresses the caller passes (no link-time
 // dependency), or -- for the CPU tests -- two Python callables begin(k, S) / end(k, S).
 #define PY_SSIZE_T_CLEAN
@@ -31,7 +31,7 @@ constexpr int kN = 13;                       // unconstrained parameters
 constexpr int kPts = kN + 1;                 // points per function+gradient request
 constexpr int kExpCols[10] = {0, 1, 2, 3, 5, 6, 7, 8, 10, 12};   // lbfgs_calibrator.py:62-87
 constexpr int kTanhCols[2] = {4, 9};
-constexpr int kMaxGroups = 2;
+constexpr int kMaxGroups = 4;            // include/dhcos.h DH_FG_SLOTS
 
 typedef int (*begin_fn)(void*, const void*, const double*, const double*, int, double, double, int,
                         double, int);
@@ -252,7 +252,7 @@ double as_double(PyObject* t, Py_ssize_t i) { return PyFloat_AsDouble(PyTuple_GE
 // run(device, groups, slots, starts, setulb, exp, tanh, (m, factr, pgtol, maxls, maxiter, maxfun,
 //     h, sqrt_eps))
 //   device: (begin_addr, end_addr, cancel_addr, ctx, surf, S0, r, N, L) or (begin_cb, end_cb)
-//   groups: up to two lists of ascending start ids; group k uses request slot k
+//   groups: up to kMaxGroups lists of ascending start ids; group k uses request slot k
 //   slots:  per group (x [s_max 13], model [2 s_max 13], f [s_max], g [s_max 13], low [s_max],
 //           exp_views, tanh_views)
 //   starts: per start (x, lo, up, nbd, wa, iwa, task, lsave, isave, dsave, ln_task, g_scratch),
@@ -302,7 +302,7 @@ PyObject* run(PyObject*, PyObject* args) {
     const int G = (int)PyList_GET_SIZE(groups);
     const int n = (int)PyList_GET_SIZE(starts_in);
     if (G < 1 || G > kMaxGroups || PyList_GET_SIZE(slots_in) != G) {
-        PyErr_SetString(PyExc_ValueError, "one or two groups, one slot each");
+        PyErr_SetString(PyExc_ValueError, "1 .. 4 groups, one slot each");
         return nullptr;
     }
     Buffers B;

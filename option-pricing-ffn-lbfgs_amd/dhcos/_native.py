@@ -26,6 +26,7 @@ MAX_N = 2048                   # longest series of the table (fast) path (DH_MAX
 MAX_N_PER_TERM = 65536         # longest accepted; longer than MAX_N runs the per-term path
 STRIKE_ABSOLUTE = 0
 STRIKE_PCT_SPOT = 1
+FG_SLOTS = 4                   # request slots of dh_surface_fg_begin / _end (DH_FG_SLOTS)
 PATH_AUTO, PATH_SPLIT, PATH_FUSED, PATH_GEN = 0, 1, 2, 3   # PATH_GEN: reported only (AUTO)
 STAMPS_PER_BLOCK = 32          # kStamps of the DH_STAMPS build (csrc/dh_kernels.hip)
 
@@ -192,9 +193,9 @@ class Context:
         self._h = h
         self.device = int(device)
         self._lock = threading.Lock()
-        # the two request slots of dh_surface_fg_begin / _end belong to the context: the start
+        # the request slots of dh_surface_fg_begin / _end belong to the context: the start
         # count of the request in flight in each (None = idle), which sizes fg_end's outputs
-        self._fg_s = [None, None]
+        self._fg_s = [None] * FG_SLOTS
 
     @property
     def handle(self):
@@ -485,8 +486,8 @@ class Surface:
         return f, g, low
 
     def fg_begin(self, X0, S0, r, N=128, L=10.0, model=None, slot=0):
-        """dh_surface_fg_begin: enqueue fg(X0) into slot 0 or 1 and return at once; the slot
-        keeps the request until fg_end(slot)."""
+        """dh_surface_fg_begin: enqueue fg(X0) into a slot (0 .. FG_SLOTS - 1) and return at
+        once; the slot keeps the request until fg_end(slot)."""
         X0 = _f64(X0).reshape(-1, 13)
         S = X0.shape[0]
         if model is not None:
@@ -503,7 +504,7 @@ class Surface:
         """dh_surface_fg_end: wait for slot's request -> (f [S], g [S, 13], low [S]).  The slot
         must hold a request this surface enqueued (the library checks the surface and S)."""
         with self.ctx._lock:
-            S = self.ctx._fg_s[int(slot)] if 0 <= int(slot) <= 1 else None
+            S = self.ctx._fg_s[int(slot)] if 0 <= int(slot) < FG_SLOTS else None
             S = 0 if S is None else S          # an idle slot: the library reports the error
             f, g, low = np.empty(S), np.empty((S, 13)), np.empty(S)
             _check(load().dh_surface_fg_end(self.ctx.handle, self._h, int(slot), S, f.ctypes.data,
@@ -535,8 +536,8 @@ class FgChannel:
     def __init__(self, surf: "Surface", slot: int, s_max: int, S0, r, N=128, L=10.0):
         lib = load()
         self.surf, self.slot, self.s_max = surf, int(slot), int(s_max)
-        if self.slot not in (0, 1) or self.s_max < 1:
-            raise ValueError("slot must be 0 or 1 and s_max >= 1")
+        if not 0 <= self.slot < FG_SLOTS or self.s_max < 1:
+            raise ValueError(f"slot must be 0 .. {FG_SLOTS - 1} and s_max >= 1")
         self._x = np.empty((self.s_max, 13))
         self._m = np.empty(2 * self.s_max * 13)        # [2][S][13] for the request's S
         self._f, self._low = np.empty(self.s_max), np.empty(self.s_max)

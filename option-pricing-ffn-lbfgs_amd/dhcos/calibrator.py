@@ -535,8 +535,8 @@ def _native_surface(cal, group_starts):
 
 
 def _pipeline_surface(cal, n_starts, force=None):
-    """The surface the two-group pipelined loop may use, or None: one start, no native channel
-    for half the starts (_native_surface), or force False ($DHCOS_SCIPY_PIPELINE = 0 when force is
+    """The surface the pipelined loop may use, or None: one start, no native channel for half
+    the starts (_native_surface; more groups hold fewer), or force False ($DHCOS_SCIPY_PIPELINE = 0 when force is
     None) keep the lockstep loop.  Round 4 measured the pipeline ahead on every bench surface once
     both loops drive prepared slots (C1 calibrate(300, 3) 5.0 vs 5.6 ms, C2 6.0 vs 6.8 ms)."""
     if force is None:
@@ -544,6 +544,19 @@ def _pipeline_surface(cal, n_starts, force=None):
     if force is False or n_starts < 2:
         return None
     return _native_surface(cal, -(-n_starts // 2))
+
+
+def _pipeline_groups(surf, n_starts):
+    """How many groups (request slots) the pipelined loop splits the starts into: every start its
+    own group, up to _native.FG_SLOTS, while a request of all starts stays within two rounds of
+    resident blocks (14 n x tiles <= 2,048: C1, C2), else two (C3: four smaller launches per round
+    would cost device time, ~11 us of fill and drain each).  $DHCOS_SCIPY_GROUPS overrides."""
+    env = os.environ.get("DHCOS_SCIPY_GROUPS", "")
+    if env:
+        return max(1, min(int(env), n_starts, _native.FG_SLOTS))
+    if (N_PARAMS + 1) * n_starts * max(1, surf.n_tiles) <= 2048:
+        return min(n_starts, _native.FG_SLOTS)
+    return min(n_starts, 2)
 
 
 def _native_async_max_sets():
@@ -572,11 +585,13 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
     with _single_threaded_blas():
         loop = _scipy_loop()
         if surf is not None:
+            G = _pipeline_groups(surf, n)
+            groups = [list(range(k, n, G)) for k in range(G)]
+            cal.pipeline_groups = groups
             if loop is not None:
-                _run_native(loop, cal, surf, x0s, [list(range(0, n, 2)), list(range(1, n, 2))],
-                            maxiter, states, outcomes)
+                _run_native(loop, cal, surf, x0s, groups, maxiter, states, outcomes)
             else:
-                _advance_pipelined(cal, surf, gens, states, outcomes)
+                _advance_pipelined(cal, surf, gens, states, outcomes, groups)
         else:
             nsurf = _native_surface(cal, max(len(g) for g in order)) if loop else None
             if nsurf is not None:
@@ -712,22 +727,22 @@ def _consume(states, gens, pending, outcomes, ids, f0, G, lows):
             del pending[sid]
 
 
-def _advance_pipelined(cal, surf, gens, states, outcomes):
-    """run_starts' two-group loop: starts of even and odd index form groups 0 and 1, each with
-    its own request slot (dh_surface_fg_begin / _end).  Group k's results are consumed, its next
-    request enqueued behind the other group's, then the other group's results are awaited: the
-    host's setulb steps of one group overlap the device's request of the other.  The per-start
-    values and bookkeeping are _advance's."""
+def _advance_pipelined(cal, surf, gens, states, outcomes, groups):
+    """run_starts' pipelined loop: group k (_pipeline_groups) on request slot k
+    (dh_surface_fg_begin / _end).  Group k's results are consumed, its next request enqueued
+    behind the other groups', then the next group's results are awaited: the host's setulb steps
+    of one group overlap the device's requests of the others.  The per-start values and
+    bookkeeping are _advance's."""
     n = len(gens)
-    groups = [[s for s in range(n) if s % 2 == k] for k in (0, 1)]
+    G = len(groups)
     pending = {sid: next(gens[sid]) for sid in range(n)}
-    inflight = [None, None]
-    busy = [False, False]              # slot k holds a request of this loop (fg_begin .. fg_end)
+    inflight = [None] * G
+    busy = [False] * G                 # slot k holds a request of this loop (fg_begin .. fg_end)
     launches = 0
     # the two slots with their arguments prepared once (_native.FgChannel: the per-request host
     # path is a row copy in, one foreign call each way, three small copies out)
     chans = [_native.FgChannel(surf, k, max(1, len(groups[k])), cal.spot, cal.risk_free_rate,
-                               cal.N) for k in (0, 1)]
+                               cal.N) for k in range(G)]
 
     def submit(k):
         ids = [sid for sid in groups[k] if sid in pending]
@@ -760,10 +775,10 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
     # the slots belong to the surface's context (the per-thread default context): whatever ends
     # this loop -- an error, a KeyboardInterrupt -- must leave no request in flight in them
     try:
-        submit(0)
-        submit(1)
-        while inflight[0] is not None or inflight[1] is not None:
-            for k in (0, 1):
+        for k in range(G):
+            submit(k)
+        while any(f is not None for f in inflight):
+            for k in range(G):
                 ids = inflight[k]
                 if ids is None:
                     continue
@@ -774,7 +789,7 @@ def _advance_pipelined(cal, surf, gens, states, outcomes):
                 _consume(states, gens, pending, outcomes, ids, f0, G, lows)
                 submit(k)
     finally:
-        for k in (0, 1):
+        for k in range(G):
             if busy[k]:
                 try:
                     surf.ctx.fg_cancel(k)

@@ -489,7 +489,8 @@ def test_lockstep_equals_sequential(dh, calib_golden):
             assert ra.message == r.message and ra.nfev == r.nfev
     nfev = [r.nfev for r, _ in a]
     assert launches == max(nfev)                       # one launch per lockstep round
-    assert p_launches == max(nfev[0::2]) + max(nfev[1::2])   # one per group round
+    # one launch per group round (run_starts' groups: _pipeline_groups)
+    assert p_launches == sum(max(nfev[s] for s in gr) for gr in cal.pipeline_groups)
 
 
 @pytest.mark.parametrize("mode", ["pipelined", "lockstep", "sequential"])
@@ -538,7 +539,7 @@ def test_fg_begin_end_slots(dh, calib_golden):
     with pytest.raises(_native.NativeError):
         surf.fg_end(0)
     with pytest.raises(_native.NativeError):
-        surf.fg_begin(A, 100.0, 0.05, 128, slot=2)
+        surf.fg_begin(A, 100.0, 0.05, 128, slot=_native.FG_SLOTS)
     for got, Xi in ((fa, A), (fb, B)):
         want = surf.fg(Xi, 100.0, 0.05, 128, model=fd_models(Xi))
         for u, v in zip(got, want):

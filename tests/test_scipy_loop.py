@@ -113,12 +113,12 @@ def _same(res, want):
         (want.nit, want.nfev, want.njev, want.status, want.success, want.message)
 
 
-@pytest.mark.parametrize("n,maxiter,pipelined", [(3, 300, True), (3, 300, False), (1, 300, False),
-                                                 (4, 5, True), (5, 300, True)])
-def test_native_loop_equals_python_loop(n, maxiter, pipelined):
+@pytest.mark.parametrize("n,maxiter,G", [(3, 300, 2), (3, 300, 3), (3, 300, 1), (1, 300, 1),
+                                         (4, 5, 2), (5, 300, 2), (6, 300, 4)])
+def test_native_loop_equals_python_loop(n, maxiter, G):
+    """G groups of starts on G request slots (run_starts' pipelined loop; G = 1: lockstep)."""
     x0s = _starts(n, 7 + n)
-    groups = ([list(range(0, n, 2)), list(range(1, n, 2))] if pipelined and n > 1
-              else [list(range(n))])
+    groups = [list(range(k, n, G)) for k in range(G)]
     outcomes, states, launches = _native(x0s, groups, maxiter)
     reqs = []
     for s, x0 in enumerate(x0s):
