@@ -92,7 +92,7 @@ struct PriceArgs {
     int partials_only;      // 1: loss requests of the device L-BFGS-B: every task stores its partial
                             // (invalid flag in the sign bit) and ends (no hand-off); the step
                             // kernel forms the sums.  2: multi-round fused requests: every task
-                            // stores its partial and invalid count and ends; loss_partials_kernel
+                            // stores its (partial, invalid count) pair and ends; loss_partials_kernel
                             // then forms the sums as the hand-off's last task would
     int M;                  // options in the (sorted) option arrays
     int N;
@@ -1287,11 +1287,9 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     const double f = nb;
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
-    if (A.partials_only == 2) {     // plain stores: loss_partials_kernel reads them next
-        if (t == 0) {
-            A.part_sse[task] = s;
-            A.part_bad[task] = (int)f;
-        }
+    if (A.partials_only == 2) {     // one plain 16-byte store (one line write per block):
+        // loss_partials_kernel reads the (partial, invalid count) pairs next
+        if (t == 0) reinterpret_cast<double2*>(A.part_sse)[task] = make_double2(s, f);
         return;
     }
     if (A.partials_only) {          // plain stores: the next launch (the step kernel) reads them;
@@ -1330,8 +1328,7 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
 // block per param set): the same reads in the same order and the same butterfly, so the same bits
 // as task_loss.  A multi-round fused grid's blocks then end with plain stores instead of the
 // agent-scope store drain and the ticket atomic (~1.8k cycles of every block's chain).
-__global__ __launch_bounds__(64) void loss_partials_kernel(const double* __restrict__ part_sse,
-                                                           const int* __restrict__ part_bad,
+__global__ __launch_bounds__(64) void loss_partials_kernel(const double2* __restrict__ part,
                                                            int n_tiles, double* sse, int* n_bad,
                                                            unsigned* done_flag, unsigned done_epoch) {
     const int64_t p = blockIdx.x;
@@ -1339,8 +1336,9 @@ __global__ __launch_bounds__(64) void loss_partials_kernel(const double* __restr
     const int64_t base_i = p * n_tiles;
     double acc = 0.0, bad = 0.0;
     for (int j = t; j < n_tiles; j += 64) {
-        acc += part_sse[base_i + j];
-        bad += part_bad[base_i + j];
+        const double2 v = part[base_i + j];
+        acc += v.x;
+        bad += v.y;
     }
     acc = xor_sum(acc, 64);
     bad = xor_sum(bad, 64);
@@ -2874,7 +2872,12 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
                 const char* e = std::getenv("DHCOS_DEFER");
                 ctx->defer_on = (e && e[0] == '0') ? 0 : 1;
             }
-            if (ctx->defer_on && A.part_sse && !A.partials_only && !A.paired) A.partials_only = 2;
+            if (ctx->defer_on && A.part_sse && !A.partials_only && !A.paired) {
+                // (partial, invalid count) pairs: 16 bytes per task
+                HIP_TRY(ctx->part_sse.reserve((size_t)A.P * A.n_tiles * 2 * sizeof(double)));
+                A.part_sse = (double*)ctx->part_sse.ptr;
+                A.partials_only = 2;
+            }
         }
     }
     if (blocks >= kPrologueKernelMinBlocks && !ctx->stamps_on) {
@@ -2908,8 +2911,8 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     HIP_TRY(hipGetLastError());
     if (A.partials_only == 2) {
         hipLaunchKernelGGL(loss_partials_kernel, dim3((unsigned)A.P), dim3(64), 0, st,
-                           (const double*)A.part_sse, (const int*)A.part_bad, A.n_tiles, A.sse,
-                           A.n_bad, A.done_flag, A.done_epoch);
+                           (const double2*)A.part_sse, A.n_tiles, A.sse, A.n_bad, A.done_flag,
+                           A.done_epoch);
         HIP_TRY(hipGetLastError());
     }
     return DH_OK;
