@@ -734,15 +734,15 @@ def _advance_pipelined(cal, surf, gens, states, outcomes, groups):
     of one group overlap the device's requests of the others.  The per-start values and
     bookkeeping are _advance's."""
     n = len(gens)
-    G = len(groups)
+    n_groups = len(groups)
     pending = {sid: next(gens[sid]) for sid in range(n)}
-    inflight = [None] * G
-    busy = [False] * G                 # slot k holds a request of this loop (fg_begin .. fg_end)
+    inflight = [None] * n_groups
+    busy = [False] * n_groups          # slot k holds a request of this loop (fg_begin .. fg_end)
     launches = 0
     # the two slots with their arguments prepared once (_native.FgChannel: the per-request host
     # path is a row copy in, one foreign call each way, three small copies out)
     chans = [_native.FgChannel(surf, k, max(1, len(groups[k])), cal.spot, cal.risk_free_rate,
-                               cal.N) for k in range(G)]
+                               cal.N) for k in range(n_groups)]
 
     def submit(k):
         ids = [sid for sid in groups[k] if sid in pending]
@@ -775,10 +775,10 @@ def _advance_pipelined(cal, surf, gens, states, outcomes, groups):
     # the slots belong to the surface's context (the per-thread default context): whatever ends
     # this loop -- an error, a KeyboardInterrupt -- must leave no request in flight in them
     try:
-        for k in range(G):
+        for k in range(n_groups):
             submit(k)
         while any(f is not None for f in inflight):
-            for k in range(G):
+            for k in range(n_groups):
                 ids = inflight[k]
                 if ids is None:
                     continue
@@ -789,7 +789,7 @@ def _advance_pipelined(cal, surf, gens, states, outcomes, groups):
                 _consume(states, gens, pending, outcomes, ids, f0, G, lows)
                 submit(k)
     finally:
-        for k in range(G):
+        for k in range(n_groups):
             if busy[k]:
                 try:
                     surf.ctx.fg_cancel(k)
