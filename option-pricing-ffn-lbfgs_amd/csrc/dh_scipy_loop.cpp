@@ -109,6 +109,9 @@ int advance(Start& s, const Loop& L) {
             return -2;
         }
         Py_DECREF(r);
+        // the loop's g is the array setulb received (g.astype makes it): setulb writes it when a
+        // line search fails (it restores the previous iterate's gradient)
+        std::memcpy(s.g, s.gs, sizeof(s.g));
         const int t = s.task[0];
         if (t == 3) {                        // FG: ScalarFunction.fun_and_grad
             bool same = true;

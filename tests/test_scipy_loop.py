@@ -19,8 +19,12 @@ SCALE = np.array([0.01, 1.0, 0.01, 0.1, 0.2, 0.01, 0.3, 0.01, 0.05, 0.2, 0.05, 0
 
 def _losses(P, invalid_above=None):
     """A synthetic loss of model params [k, 13]: weighted squares plus a ripple; 1e10 (the
-    reference's invalid-price loss) where P[:, 1] exceeds invalid_above."""
+    reference's invalid-price loss) where P[:, 1] exceeds invalid_above.  invalid_above = "kink":
+    weighted absolute values plus a smooth part instead (a kink at TARGET, where the line search
+    fails; the gradient differs from point to point, so a restored one is told apart)."""
     z = (P - TARGET) / SCALE
+    if isinstance(invalid_above, str):
+        return np.sum(np.abs(z), axis=1) + 1e-3 * np.sum(z * z + z, axis=1)
     f = np.sum(z * z, axis=1) * 1e-3 + 1e-4 * np.sin(3.0 * P[:, 0] / SCALE[0])
     if invalid_above is not None:
         f = np.where(P[:, 1] > invalid_above, INVALID, f)
@@ -48,7 +52,7 @@ def _bits(a):
     return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
 
 
-def _native(x0s, groups, maxiter, invalid_above=None):
+def _native(x0s, groups, maxiter, invalid_above=None, setulb=None):
     loop = CM._scipy_loop()
     assert loop is not None, "dhcos._scipy_loop is built with the library (csrc/Makefile)"
     arrs = [CM._lbfgsb_arrays(x0) for x0 in x0s]
@@ -70,8 +74,8 @@ def _native(x0s, groups, maxiter, invalid_above=None):
         seen.append((k, S))
 
     rc, launches, evals, rows = loop.run((begin, lambda k, S: None), [list(g) for g in groups],
-                                         slots, arrs, CM._lbfgsb.setulb, np.exp, np.tanh,
-                                         CM._loop_consts(maxiter))
+                                         slots, arrs, setulb or CM._lbfgsb.setulb, np.exp,
+                                         np.tanh, CM._loop_consts(maxiter))
     assert rc == 0 and launches == len(seen)
     assert evals == 14 * sum(S for _, S in seen)
     states = [CM._StartState() for _ in x0s]
@@ -141,6 +145,38 @@ def test_native_loop_invalid_losses_and_sequential_groups():
         want, n_calls, best, req = _python(x0, 300, invalid_above=2.5)
         _same(outcomes[0][0], want)
         assert (states[0].n_calls, states[0].best_loss, launches) == (n_calls, best, req)
+
+
+def test_native_loop_line_search_failure():
+    """A start on a kink: the line search fails (ABNORMAL), setulb restores the previous iterate's
+    x and gradient in its arrays, and the result carries them as lbfgsb_steps' does."""
+    x0 = CM.DoubleHestonJumpCalibrator.inverse_transform_params(None, dict(zip(CM.PARAM_NAMES,
+                                                                               TARGET)))
+    outcomes, states, launches = _native([x0, x0 + 0.01], [[0], [1]], 300, invalid_above="kink")
+    for s, x in enumerate([x0, x0 + 0.01]):
+        want, n_calls, best, req = _python(x, 300, invalid_above="kink")
+        _same(outcomes[s][0], want)
+        assert (states[s].n_calls, states[s].best_loss) == (n_calls, best)
+    assert outcomes[0][0].message.startswith("ABNORMAL")
+
+
+def test_native_loop_keeps_what_setulb_writes_into_g(monkeypatch):
+    """setulb may write the g it receives (on a failed line search it restores the previous
+    iterate's gradient there), and lbfgsb_steps keeps that array as its g.  A setulb that scales g
+    after every NEW_X step makes any difference in that bookkeeping change the trajectory."""
+    real = CM._lbfgsb.setulb
+
+    def setulb(*a):
+        real(*a)
+        if a[11][0] == 1:                        # task NEW_X
+            np.multiply(a[6], 1.0 + 2.0 ** -20, out=a[6])
+
+    x0s = _starts(2, 13)
+    outcomes, states, launches = _native(x0s, [[0], [1]], 300, setulb=setulb)
+    monkeypatch.setattr(CM._lbfgsb, "setulb", setulb)
+    for s, x0 in enumerate(x0s):
+        want, n_calls, best, req = _python(x0, 300)
+        _same(outcomes[s][0], want)
 
 
 def test_native_loop_vanishing_step():
