@@ -645,25 +645,28 @@ def test_fg_slots_belong_to_the_context(dh, calib_golden):
         assert np.array_equal(u, v)
 
 
-def test_pipelined_driver_interrupted_leaves_context_usable(dh, calib_golden, monkeypatch):
-    """An interrupt inside the two-group pipeline (here: a KeyboardInterrupt from the per-request
-    transforms while the other group's request is in flight) must not leave a slot busy on the
-    thread's cached context: the next calibrate on it runs and gives the uninterrupted result."""
+@pytest.mark.parametrize("native", ["1", "0"])
+def test_pipelined_driver_interrupted_leaves_context_usable(dh, calib_golden, monkeypatch, native):
+    """An interrupt inside the pipelined loop (here: a KeyboardInterrupt from SciPy's setulb while
+    other groups' requests are in flight), in the native loop and in the Python one, must not leave
+    a slot busy on the thread's cached context: the next calibrate on it runs and gives the
+    uninterrupted result."""
     import dhcos.calibrator as CM
+    monkeypatch.setenv("DHCOS_NATIVE_LOOP", native)
     g = calib_golden
     x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
     want = CM.run_starts(dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"]), x0s, 300)
-    real, calls = CM.fd_models, [0]
+    real, calls = CM._lbfgsb.setulb, [0]
 
-    def flaky(X0, *a, **k):
+    def flaky(*a):
         calls[0] += 1
-        if calls[0] == 5:
+        if calls[0] == 9:
             raise KeyboardInterrupt
-        return real(X0, *a, **k)
-    monkeypatch.setattr(CM, "fd_models", flaky)
+        return real(*a)
+    monkeypatch.setattr(CM._lbfgsb, "setulb", flaky)
     with pytest.raises(KeyboardInterrupt):
         CM.run_starts(dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"]), x0s, 300)
-    monkeypatch.setattr(CM, "fd_models", real)
+    monkeypatch.setattr(CM._lbfgsb, "setulb", real)
     got = CM.run_starts(dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"]), x0s, 300)
     for (a, _), (b, _) in zip(got, want):
         assert np.array_equal(a.x, b.x) and a.fun == b.fun and a.nit == b.nit
