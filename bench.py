@@ -362,6 +362,9 @@ def _max_over_ranks(dt, world, coll):
     return dt
 
 
+PREWARM_S = 0.25          # untimed back-to-back requests before the warm-up steps (request_bench)
+
+
 def event_ms(run, stream, reps):
     """Median HIP-event time (ms) of run(j) on `stream`, one isolated call per event pair."""
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -539,6 +542,17 @@ def request_bench(cfg, steps, warmup, world, rank, dev, coll, stream, starts_ran
     for i in range(n_host):
         surf.loss_terms(host[i % n_rows], N)
     host_rate = prices_per_step * n_host / (time.perf_counter() - t0)
+    # then device requests back to back for PREWARM_S of wall time (untimed, before the W warm-up
+    # steps): an idle MI355X takes tens of ms to reach its sustained clock, and a 20-step timed
+    # region (~1.2 ms on C3) right after a few ms of work measured 63.8 us per step against
+    # 59.0 us sustained (round 5)
+    n_pre = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < PREWARM_S:
+        for _ in range(16):
+            run(steps + n_pre % max(warmup, 1))
+            n_pre += 1
+        torch.cuda.synchronize()
 
     def timed(k):
         for i in range(warmup):
@@ -558,6 +572,7 @@ def request_bench(cfg, steps, warmup, world, rank, dev, coll, stream, starts_ran
             "ms_per_step": dt / steps * 1e3, "ker_ms": ker_ms, "S": S, "M": M, "N": N,
             "prices_per_step": prices_per_step, "opts": opts, "S0": S0, "r": r, "surf": surf,
             "host_rate": host_rate, "timed": timed, "run": run, "steps": steps,
+            "prewarm_requests": n_pre,
             "groups": len({o["maturity"] for o in opts}), "n_tiles": surf.n_tiles}
 
 
@@ -764,6 +779,9 @@ def main():
                        "parallelism": f"independent requests per rank x{world}"},
             "roofline": roofline,
             "host_api_prices_per_sec": q["host_rate"],
+            "prewarm": {"seconds": PREWARM_S, "requests": q["prewarm_requests"],
+                        "note": "untimed device requests before the warm-up steps, to the "
+                                "sustained clock"},
         }
         line.update(side)
         if calib:

@@ -125,11 +125,6 @@ struct PriceArgs {
     unsigned* ahead_flag;
     int ahead_stride;       // 0: off
     unsigned ahead_epoch;
-    // host-visible completion (dh_surface_fg_begin's requests): the writer of sse[p] / n_bad[p]
-    // then sets done_flag[p] = done_epoch with a system-scope release, in mapped host memory the
-    // host polls instead of an event (nullptr: off)
-    unsigned* done_flag;
-    unsigned done_epoch;
 };
 
 // w_k of table q sits at table_w(A, q)[k * table_step(A)].  The small-tile option kernel has one
@@ -1262,12 +1257,6 @@ __device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int 
 // the partial with agent-scope (sc1, write-through) stores, drains them with s_waitcnt vmcnt(0),
 // then adds to p's counter; in the wave whose add returns n_tiles - 1 every lane reads partials
 // of p with sc1 loads, the wave sums them in a fixed order and resets the counter.
-// sse[p] / n_bad[p] are written (by this thread): post p's completion to the host.  The release
-// at system scope orders those stores (mapped host memory) before the flag's (a vector store).
-__device__ __forceinline__ void post_done(unsigned* done_flag, unsigned epoch, int64_t p) {
-    if (done_flag) __hip_atomic_store(&done_flag[p], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t task, int nopt,
                                           int t, const double* lsse, const double* lbad) {
     DH_STAMP(A, 13);
@@ -1320,7 +1309,6 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
         A.sse[p] = acc;
         A.n_bad[p] = (int)bad;
         __hip_atomic_store(&A.counter[p * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        post_done(A.done_flag, A.done_epoch, p);
     }
 }
 
@@ -1329,8 +1317,7 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
 // as task_loss.  A multi-round fused grid's blocks then end with plain stores instead of the
 // agent-scope store drain and the ticket atomic (~1.8k cycles of every block's chain).
 __global__ __launch_bounds__(64) void loss_partials_kernel(const double2* __restrict__ part,
-                                                           int n_tiles, double* sse, int* n_bad,
-                                                           unsigned* done_flag, unsigned done_epoch) {
+                                                           int n_tiles, double* sse, int* n_bad) {
     const int64_t p = blockIdx.x;
     const int t = threadIdx.x;
     const int64_t base_i = p * n_tiles;
@@ -1345,7 +1332,6 @@ __global__ __launch_bounds__(64) void loss_partials_kernel(const double2* __rest
     if (t == 0) {
         sse[p] = acc;
         n_bad[p] = (int)bad;
-        post_done(done_flag, done_epoch, p);
     }
 }
 
@@ -1812,7 +1798,6 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A_, 
     A.sse[p] = acc;
     A.n_bad[p] = bad;
     __hip_atomic_store(&A.counter[p * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    post_done(A.done_flag, A.done_epoch, p);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -2058,7 +2043,6 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
                     A.sse[pp] = s2;
                     A.n_bad[pp] = bad;
                     __hip_atomic_store(&A.counter[pp * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    post_done(A.done_flag, A.done_epoch, pp);
                 }
             }
         }
@@ -2619,17 +2603,7 @@ struct dh_ctx {
         const dh_surface* surf = nullptr;   // the surface the request was enqueued on
         bool pending = false;
         hipEvent_t done = nullptr;
-        // completion by flags (PriceArgs::done_flag): [P] words in mapped host memory, set to the
-        // slot's request epoch by the kernels; flag_armed: this request posts them (no event)
-        HostBuf h_flag;
-        unsigned flag_epoch = 0;
-        bool flag_armed = false;
     } fg[DH_FG_SLOTS];
-    // the flags the next loss launch posts (set by dh_surface_fg_begin around its launch) and
-    // $DHCOS_FG_FLAG (-1: not read yet; 0: completion by events instead)
-    unsigned* fg_done_arm = nullptr;
-    unsigned fg_done_epoch = 0;
-    int fg_flag_on = -1;
     DevBuf lb_trace, lb_trace_n;   // diagnostic request trace of dh_calibrate_lbfgs
     hipEvent_t lb_ev[2] = {nullptr, nullptr};   // chunk-completion events of dh_calibrate_lbfgs
     int64_t lb_trace_cap = 0;
@@ -2911,8 +2885,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     HIP_TRY(hipGetLastError());
     if (A.partials_only == 2) {
         hipLaunchKernelGGL(loss_partials_kernel, dim3((unsigned)A.P), dim3(64), 0, st,
-                           (const double2*)A.part_sse, A.n_tiles, A.sse, A.n_bad, A.done_flag,
-                           A.done_epoch);
+                           (const double2*)A.part_sse, A.n_tiles, A.sse, A.n_bad);
         HIP_TRY(hipGetLastError());
     }
     return DH_OK;
@@ -3131,7 +3104,6 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     for (auto& F : ctx->fg) {
         F.h_params.release();
         F.h_loss.release();
-        F.h_flag.release();
         if (F.done) (void)hipEventDestroy(F.done);
     }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -3384,8 +3356,6 @@ static int surface_loss_launch(dh_ctx* ctx, const dh_surface* s, const double* d
     A.n_bad = (int*)d_n_bad;
     A.live_count = live_count;
     A.partials_only = partials_only && !A.exact ? 1 : 0;
-    A.done_flag = ctx->fg_done_arm;
-    A.done_epoch = ctx->fg_done_epoch;
     return launch_price(ctx, A, st);
 }
 
@@ -4580,37 +4550,17 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     F.S = S;
     F.M = s->M;
     F.surf = s;
-    F.flag_armed = false;
     if (S == 0) {
         HIP_TRY(hipEventRecord(F.done, ctx->stream));
         F.pending = true;
         return DH_OK;
     }
-    // completion by flags: every param set's loss writer posts the slot's epoch (the slot is idle,
-    // so no kernel of its previous request writes these words any more)
-    if (ctx->fg_flag_on < 0) {
-        const char* e = std::getenv("DHCOS_FG_FLAG");
-        ctx->fg_flag_on = (e && e[0] == '0') ? 0 : 1;
-    }
-    const bool flags = ctx->fg_flag_on != 0;
-    if (flags) {
-        const size_t cap0 = F.h_flag.cap;
-        HIP_TRY(F.h_flag.reserve(P * sizeof(unsigned)));
-        if (F.h_flag.cap != cap0 || ++F.flag_epoch == 0) {
-            std::memset(F.h_flag.ptr, 0, F.h_flag.cap);
-            F.flag_epoch = 1;
-        }
-        ctx->fg_done_arm = (unsigned*)F.h_flag.dptr;
-        ctx->fg_done_epoch = F.flag_epoch;
-    }
     fg_points(x0, model, S, S0, r, (double*)F.h_params.ptr, F.pen.data(), F.dx.data());
     rc = dh_surface_loss_dev(ctx, s, (const double*)F.h_params.dptr, (int)P, N, L,
                              (double*)F.h_loss.dptr, (int32_t*)((double*)F.h_loss.dptr + P),
                              nullptr, ctx->stream);
-    ctx->fg_done_arm = nullptr;
     if (rc) return rc;
-    if (!flags) HIP_TRY(hipEventRecord(F.done, ctx->stream));
-    F.flag_armed = flags;
+    HIP_TRY(hipEventRecord(F.done, ctx->stream));
     F.pending = true;
     return DH_OK;
 }
@@ -4631,34 +4581,12 @@ extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, int
     DeviceScope dev_scope(ctx->device);
     if (dev_scope.rc) return dev_scope.rc;
     const size_t P = (size_t)F.S * dhlb::kPts;
-    if (F.flag_armed) {
-        // busy-wait on the param sets' flags in order (each holds the request's epoch once its
-        // sse / n_bad are visible); the stream's state is checked now and then, so a request
-        // whose flags never come (none known) still ends once the stream is idle
-        const unsigned* fl = (const unsigned*)F.h_flag.ptr;
-        unsigned spins = 0;
-        for (size_t i = 0; i < P;) {
-            if (__atomic_load_n(&fl[i], __ATOMIC_ACQUIRE) == F.flag_epoch) {
-                ++i;
-                continue;
-            }
-            if ((++spins & 1023u) == 0) {
-                const hipError_t e = hipStreamQuery(ctx->stream);
-                if (e == hipSuccess) break;
-                if (e != hipErrorNotReady) {
-                    F.pending = false;
-                    return fail(DH_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
-                }
-            }
-        }
-    } else {
-        for (;;) {                      // busy-wait: an optimizer iteration waits on it
-            const hipError_t e = hipEventQuery(F.done);
-            if (e == hipSuccess) break;
-            if (e != hipErrorNotReady) {
-                F.pending = false;
-                return fail(DH_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
-            }
+    for (;;) {                          // busy-wait: an optimizer iteration waits on it
+        const hipError_t e = hipEventQuery(F.done);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) {
+            F.pending = false;
+            return fail(DH_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
         }
     }
     F.pending = false;
@@ -4675,7 +4603,7 @@ extern "C" int dh_surface_fg_cancel(dh_ctx* ctx, int slot) {
     DeviceScope dev_scope(ctx->device);
     if (dev_scope.rc) return dev_scope.rc;
     F.pending = false;                  // cleared even if the wait fails: the slot is usable again
-    HIP_TRY(F.flag_armed ? hipStreamSynchronize(ctx->stream) : hipEventSynchronize(F.done));
+    HIP_TRY(hipEventSynchronize(F.done));
     return DH_OK;
 }
 

@@ -547,16 +547,14 @@ def _pipeline_surface(cal, n_starts, force=None):
 
 
 def _pipeline_groups(surf, n_starts):
-    """How many groups (request slots) the pipelined loop splits the starts into: every start its
-    own group, up to _native.FG_SLOTS, while a request of all starts stays within two rounds of
-    resident blocks (14 n x tiles <= 2,048: C1, C2), else two (C3: four smaller launches per round
-    would cost device time, ~11 us of fill and drain each).  $DHCOS_SCIPY_GROUPS overrides."""
+    """How many groups (request slots) the pipelined loop splits the starts into: two, or
+    $DHCOS_SCIPY_GROUPS (up to _native.FG_SLOTS).  Measured with the native loop (round 5,
+    calibrate(300, 3)): every start on its own slot is slower than two groups on C1 (4.72 vs
+    4.42 ms) and C2 (6.24 vs 5.94 ms) -- each extra request costs the device more than the host
+    work it hides -- and C3 is device-bound."""
     env = os.environ.get("DHCOS_SCIPY_GROUPS", "")
-    if env:
-        return max(1, min(int(env), n_starts, _native.FG_SLOTS))
-    if (N_PARAMS + 1) * n_starts * max(1, surf.n_tiles) <= 2048:
-        return min(n_starts, _native.FG_SLOTS)
-    return min(n_starts, 2)
+    G = int(env) if env else 2
+    return max(1, min(G, n_starts, _native.FG_SLOTS))
 
 
 def _native_async_max_sets():

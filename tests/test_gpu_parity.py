@@ -546,43 +546,6 @@ def test_fg_begin_end_slots(dh, calib_golden):
             assert np.array_equal(u, v)
 
 
-def test_fg_completion_by_flags_equals_events(dh, calib_golden, monkeypatch):
-    """dh_surface_fg_end's two completion modes: the kernels' per-param-set flags in mapped host
-    memory (default) and a stream event ($DHCOS_FG_FLAG=0) return fg's bits, over many requests
-    alternating on both slots (the flags' epochs advance per request), on the pipelined loop's
-    3-start and single-start sizes."""
-    from dhcos import _native
-    from dhcos.calibrator import fd_models
-    g = calib_golden
-    mkt = g["test_market"]
-    X = np.array([s["x0"] for s in g["calibrate_seed0_starts"]], dtype=float)
-    got = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("DHCOS_FG_FLAG", mode)
-        ctx = _native.Context(0)
-        surf = _native.Surface(ctx, [o["strike"] for o in mkt], [o["maturity"] for o in mkt],
-                               [True] * len(mkt), [o["price"] for o in mkt])
-        out = []
-        rs = np.random.RandomState(4)
-        for i in range(24):
-            A = X + rs.normal(0, 0.02, X.shape)
-            B = A[i % 3:i % 3 + 1]
-            surf.fg_begin(A, 100.0, 0.05, 128, model=fd_models(A), slot=i % 2)
-            surf.fg_begin(B, 100.0, 0.05, 128, model=fd_models(B), slot=1 - i % 2)
-            fb = surf.fg_end(1 - i % 2)
-            fa = surf.fg_end(i % 2)
-            if i % 8 == 0:
-                want = surf.fg(A, 100.0, 0.05, 128, model=fd_models(A))
-                for u, v in zip(fa, want):
-                    assert np.array_equal(u, v)
-            out.append((fa, fb))
-        surf.close()
-        got[mode] = out
-    for (fa, fb), (ga, gb) in zip(got["1"], got["0"]):
-        for u, v in zip(fa + fb, ga + gb):
-            assert np.array_equal(u, v)
-
-
 def test_characteristic_function_complex_phi(dh, cf_complex_golden):
     """DoubleHeston.characteristic_function at complex phi (double_heston.py:48-61 documents
     phi : complex) against the reference's values: 216 scalar points (damped shifts u - i alpha,
