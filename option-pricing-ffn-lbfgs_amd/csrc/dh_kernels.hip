@@ -675,6 +675,12 @@ constexpr int kAheadRec = 16;
 #define DH_AHEAD_SKIP_STAGE 0     // 1 measured slower on C3 (58.5 vs 57.8 us kernel)
 #endif
 constexpr bool kAheadSkipStage = DH_AHEAD_SKIP_STAGE;   // the writer wave stages no options
+// The writer: the staging wave before the first barrier (0), or the cut wave during the CF loop,
+// which leaves it idle on C3's tables, right before its ahead_cut (1)
+#ifndef DH_AHEAD_ON_CUT
+#define DH_AHEAD_ON_CUT 0
+#endif
+constexpr bool kAheadOnCut = DH_AHEAD_ON_CUT;
 
 // v of lane (lane & ~7) | l: the 8-lane group's broadcast
 __device__ __forceinline__ double grp8_bcast(double v, int l) {
@@ -2099,7 +2105,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // prologues ahead (4-wave build, >= 3 waves): the first-round block's writer wave, and
     // whether this block's constants may have been formed ahead
     const int64_t R = (WV <= DH_FUSED_WAVES && nthr >= 192) ? A.ahead_stride : 0;
-    const int wahead = nthr / 64 - 2;
+    const int wahead = kAheadOnCut ? wcut : nthr / 64 - 2;
     const bool ahead_w = R > 0 && q < R;
     const bool ahead_r = R > 0 && q >= R && q < (kAheadMax + 1) * R;
     const int64_t nblocks = gridDim.x;
@@ -2158,7 +2164,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         L.xK[i] = xK;
         L.exK[i] = ratio;
     }
-    if (ahead_w && wv == wahead) ahead_write(A, H, q, nblocks, lane, ahd_ab);
+    if (!kAheadOnCut && ahead_w && wv == wahead) ahead_write(A, H, q, nblocks, lane, ahd_ab);
     __syncthreads();
     serial_prio(false);
     if (__builtin_amdgcn_readfirstlane(live_v) <= 0) return;   // every block reads the same count
@@ -2243,7 +2249,10 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     }
     // prologues ahead: the later tables' K_cf on the cut wave; both writer waves' stores drained
     // before the barrier, the flags after it
-    if (ahead_w && wv == wcut) ahead_cut(A, H, q, nblocks, lane, ahd_ab);
+    if (ahead_w && wv == wcut) {
+        if (kAheadOnCut) ahead_write(A, H, q, nblocks, lane, ahd_ab);
+        ahead_cut(A, H, q, nblocks, lane, ahd_ab);
+    }
     if (ahead_w && wv == wahead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (!kEarlyClamp) clamp_scan();
     DH_STAMP(A, 21);
@@ -4517,6 +4526,8 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     if (rc) return rc;
     rc = check_N(N);
     if (rc) return rc;
+    if (s->ctx && s->ctx->device != ctx->device)
+        return fail(DH_E_ARG, "surface and context are on different devices");
     auto& F = ctx->fg[slot];
     if (F.pending) return fail(DH_E_ARG, "slot has a request in flight (call dh_surface_fg_end)");
     const size_t P = (size_t)S * dhlb::kPts;

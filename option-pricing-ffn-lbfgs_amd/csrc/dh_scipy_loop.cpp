@@ -202,7 +202,7 @@ struct Device {
     begin_fn begin = nullptr;
     end_fn end = nullptr;
     cancel_fn cancel = nullptr;
-    void* ctx = nullptr;
+    void* ctx[kMaxGroups] = {};              // slot k's context (its stream and scratch)
     const void* surf = nullptr;
     double S0 = 0, r = 0, L = 0;
     int N = 0;
@@ -219,7 +219,7 @@ int dev_begin(Device& D, Slot& sl, int k, int S) {
     }
     int rc;
     Py_BEGIN_ALLOW_THREADS
-    rc = D.begin(D.ctx, D.surf, sl.x, sl.model, S, D.S0, D.r, D.N, D.L, k);
+    rc = D.begin(D.ctx[k], D.surf, sl.x, sl.model, S, D.S0, D.r, D.N, D.L, k);
     Py_END_ALLOW_THREADS
     return rc;
 }
@@ -233,7 +233,7 @@ int dev_end(Device& D, Slot& sl, int k, int S) {
     }
     int rc;
     Py_BEGIN_ALLOW_THREADS
-    rc = D.end(D.ctx, D.surf, k, S, sl.f, sl.g, sl.low);
+    rc = D.end(D.ctx[k], D.surf, k, S, sl.f, sl.g, sl.low);
     Py_END_ALLOW_THREADS
     return rc;
 }
@@ -244,7 +244,7 @@ void cancel_busy(Device& D, Slot* slots, int G) {
         slots[k].busy = false;
         if (D.cancel) {
             Py_BEGIN_ALLOW_THREADS
-            (void)D.cancel(D.ctx, k);
+            (void)D.cancel(D.ctx[k], k);
             Py_END_ALLOW_THREADS
         }
     }
@@ -254,7 +254,8 @@ double as_double(PyObject* t, Py_ssize_t i) { return PyFloat_AsDouble(PyTuple_GE
 
 // run(device, groups, slots, starts, setulb, exp, tanh, (m, factr, pgtol, maxls, maxiter, maxfun,
 //     h, sqrt_eps))
-//   device: (begin_addr, end_addr, cancel_addr, ctx, surf, S0, r, N, L) or (begin_cb, end_cb)
+//   device: (begin_addr, end_addr, cancel_addr, ctx, surf, S0, r, N, L) or (begin_cb, end_cb);
+//           ctx: one context handle, or a tuple with slot k's context at k
 //   groups: up to kMaxGroups lists of ascending start ids; group k uses request slot k
 //   slots:  per group (x [s_max 13], model [2 s_max 13], f [s_max], g [s_max 13], low [s_max],
 //           exp_views, tanh_views)
@@ -286,14 +287,20 @@ PyObject* run(PyObject*, PyObject* args) {
         D.begin = (begin_fn)PyLong_AsVoidPtr(PyTuple_GET_ITEM(dev, 0));
         D.end = (end_fn)PyLong_AsVoidPtr(PyTuple_GET_ITEM(dev, 1));
         D.cancel = (cancel_fn)PyLong_AsVoidPtr(PyTuple_GET_ITEM(dev, 2));
-        D.ctx = PyLong_AsVoidPtr(PyTuple_GET_ITEM(dev, 3));
+        PyObject* cx = PyTuple_GET_ITEM(dev, 3);     // one context, or one per slot
+        for (int k = 0; k < kMaxGroups; ++k) {
+            PyObject* c = PyTuple_Check(cx) ? (k < PyTuple_GET_SIZE(cx) ? PyTuple_GET_ITEM(cx, k)
+                                                                        : nullptr)
+                                            : cx;
+            D.ctx[k] = c ? PyLong_AsVoidPtr(c) : nullptr;
+        }
         D.surf = PyLong_AsVoidPtr(PyTuple_GET_ITEM(dev, 4));
         D.S0 = as_double(dev, 5);
         D.r = as_double(dev, 6);
         D.N = (int)PyLong_AsLong(PyTuple_GET_ITEM(dev, 7));
         D.L = as_double(dev, 8);
         if (PyErr_Occurred()) return nullptr;
-        if (!D.begin || !D.end || !D.cancel || !D.ctx || !D.surf) {
+        if (!D.begin || !D.end || !D.cancel || !D.ctx[0] || !D.surf) {
             PyErr_SetString(PyExc_ValueError, "null device entry point or handle");
             return nullptr;
         }
@@ -308,6 +315,12 @@ PyObject* run(PyObject*, PyObject* args) {
         PyErr_SetString(PyExc_ValueError, "1 .. 4 groups, one slot each");
         return nullptr;
     }
+    if (!D.begin_cb)
+        for (int k = 0; k < G; ++k)
+            if (!D.ctx[k]) {
+                PyErr_SetString(PyExc_ValueError, "no context for a group's slot");
+                return nullptr;
+            }
     Buffers B;
     std::vector<Start> st(n);
     for (int s = 0; s < n; ++s) {

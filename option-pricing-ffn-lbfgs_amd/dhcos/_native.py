@@ -196,6 +196,7 @@ class Context:
         # the request slots of dh_surface_fg_begin / _end belong to the context: the start
         # count of the request in flight in each (None = idle), which sizes fg_end's outputs
         self._fg_s = [None] * FG_SLOTS
+        self._settings = {}            # set_exact / set_tail_cut / set_path, for slot contexts
 
     @property
     def handle(self):
@@ -208,15 +209,18 @@ class Context:
     def set_exact(self, on: bool):
         """Validation mode: price every option by the per-term reference-order path."""
         _check(load().dh_ctx_set_exact(self._h, 1 if on else 0))
+        self._settings["set_exact"] = bool(on)
 
     def set_tail_cut(self, on: bool):
         """Adaptive tail of the angle sums (default on); off sums every term k < N."""
         _check(load().dh_ctx_set_tail_cut(self._h, 1 if on else 0))
+        self._settings["set_tail_cut"] = bool(on)
 
     def set_path(self, path: int):
         """Request kernels: PATH_AUTO (default), PATH_SPLIT (table + option launches),
         or PATH_FUSED (one launch per request where every maturity group is one tile)."""
         _check(load().dh_ctx_set_path(self._h, int(path)))
+        self._settings["set_path"] = int(path)
 
     @property
     def last_path(self) -> int:
@@ -254,6 +258,22 @@ class Context:
     def synchronize(self):
         _check(load().dh_ctx_synchronize(self._h))
 
+    def slot_context(self, k: int) -> "Context":
+        """Request slot k's context for a pipelined host driver: this context for slot 0, else a
+        context of its own on the same device, cached (its own stream and scratch, so two groups'
+        requests may run on the GPU at once), carrying this context's settings (exact mode, tail
+        cut, path)."""
+        if k == 0:
+            return self
+        cache = self.__dict__.setdefault("_slot_ctxs", {})
+        c = cache.get(k)
+        if c is None:
+            c = cache[k] = Context(self.device)
+        for name, v in self._settings.items():
+            if c._settings.get(name) != v:
+                getattr(c, name)(v)
+        return c
+
     def fg_cancel(self, slot):
         """dh_surface_fg_cancel: wait for slot's request (if any) and discard it."""
         with self._lock:
@@ -265,6 +285,8 @@ class Context:
     def close(self):
         for surf in self.__dict__.pop("_grid_surfaces", {}).values():   # generator.price_grid's
             surf.close()
+        for c in self.__dict__.pop("_slot_ctxs", {}).values():
+            c.close()
         if getattr(self, "_h", None):
             load().dh_ctx_destroy(self._h)
             self._h = None
@@ -533,9 +555,10 @@ class FgChannel:
     Surface.fg_begin / fg_end marshal every argument per call, ~10 us each).  The slot protocol
     (Context._fg_s, the context lock) is Surface.fg_begin / fg_end's."""
 
-    def __init__(self, surf: "Surface", slot: int, s_max: int, S0, r, N=128, L=10.0):
+    def __init__(self, surf: "Surface", slot: int, s_max: int, S0, r, N=128, L=10.0, ctx=None):
         lib = load()
         self.surf, self.slot, self.s_max = surf, int(slot), int(s_max)
+        self.ctx = surf.ctx if ctx is None else ctx     # the slot's context (same device)
         if not 0 <= self.slot < FG_SLOTS or self.s_max < 1:
             raise ValueError(f"slot must be 0 .. {FG_SLOTS - 1} and s_max >= 1")
         self._x = np.empty((self.s_max, 13))
@@ -546,7 +569,7 @@ class FgChannel:
         self._begin.restype, self._begin.argtypes = C.c_int, None
         self._end = lib["dh_surface_fg_end"]
         self._end.restype, self._end.argtypes = C.c_int, None
-        ctx = C.c_void_p(surf.ctx.handle.value)
+        ctx = C.c_void_p(self.ctx.handle.value)
         sh = C.c_void_p(surf.handle.value)
         self._S = C.c_int(0)
         self._bargs = (ctx, sh, C.c_void_p(self._x.ctypes.data), C.c_void_p(self._m.ctypes.data),
@@ -554,8 +577,8 @@ class FgChannel:
                        C.c_double(float(L)), C.c_int(self.slot))
         self._eargs = (ctx, sh, C.c_int(self.slot), self._S, C.c_void_p(self._f.ctypes.data),
                        C.c_void_p(self._g.ctypes.data), C.c_void_p(self._low.ctypes.data))
-        self._lock = surf.ctx._lock
-        self._fg_s = surf.ctx._fg_s
+        self._lock = self.ctx._lock
+        self._fg_s = self.ctx._fg_s
         self._consts = (float(S0), float(r), int(N), float(L))
 
     def loop_slot(self):
@@ -574,7 +597,7 @@ class FgChannel:
             return C.cast(lib[name], C.c_void_p).value
         S0, r, N, L = self._consts
         return (addr("dh_surface_fg_begin"), addr("dh_surface_fg_end"),
-                addr("dh_surface_fg_cancel"), self.surf.ctx.handle.value, self.surf.handle.value,
+                addr("dh_surface_fg_cancel"), self.ctx.handle.value, self.surf.handle.value,
                 S0, r, N, L)
 
     def model_out(self, S: int) -> np.ndarray:

@@ -22,6 +22,7 @@ What changes relative to the reference, and what does not:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 import time
@@ -557,6 +558,16 @@ def _pipeline_groups(surf, n_starts):
     return max(1, min(G, n_starts, _native.FG_SLOTS))
 
 
+def _slot_ctx(surf, k):
+    """Request slot k's context: the surface's own for slot 0; for the others, by default, a
+    context of their own on the same device (Context.slot_context: its own stream and scratch, so
+    two groups' requests may run on the GPU at once); $DHCOS_SCIPY_STREAMS=0 keeps every slot on
+    the surface's context (one stream)."""
+    if os.environ.get("DHCOS_SCIPY_STREAMS", "") == "0":
+        return surf.ctx
+    return surf.ctx.slot_context(k)
+
+
 def _native_async_max_sets():
     return 1024                        # dh_surface_fg_begin: 14 S <= 1024 (include/dhcos.h)
 
@@ -740,7 +751,7 @@ def _advance_pipelined(cal, surf, gens, states, outcomes, groups):
     # the two slots with their arguments prepared once (_native.FgChannel: the per-request host
     # path is a row copy in, one foreign call each way, three small copies out)
     chans = [_native.FgChannel(surf, k, max(1, len(groups[k])), cal.spot, cal.risk_free_rate,
-                               cal.N) for k in range(n_groups)]
+                               cal.N, ctx=_slot_ctx(surf, k)) for k in range(n_groups)]
 
     def submit(k):
         ids = [sid for sid in groups[k] if sid in pending]
@@ -790,7 +801,7 @@ def _advance_pipelined(cal, surf, gens, states, outcomes, groups):
         for k in range(n_groups):
             if busy[k]:
                 try:
-                    surf.ctx.fg_cancel(k)
+                    chans[k].ctx.fg_cancel(k)
                 except Exception:      # noqa: BLE001 -- unwinding: the first error wins
                     pass
     cal.lockstep_launches = launches
@@ -864,14 +875,20 @@ def _loop_results(rows, arrs, maxiter, states, outcomes, ids):
 
 def _run_native(loop, cal, surf, x0s, groups, maxiter, states, outcomes):
     """run_starts' request loop in native code (csrc/dh_scipy_loop.cpp): _advance_pipelined with
-    two groups, _advance's lockstep loop with one; the same setulb calls, fd_models bits and
-    per-start bookkeeping (tests/test_scipy_loop.py; tests/test_gpu_parity.py holds the two
-    loops' calibrations equal bit for bit).  The context's request slots are held for the call."""
+    several groups (each slot on its own context, _slot_ctx), _advance's lockstep loop with one;
+    the same setulb calls, fd_models bits and per-start bookkeeping (tests/test_scipy_loop.py;
+    tests/test_gpu_parity.py holds the two loops' calibrations equal bit for bit).  The contexts'
+    request slots are held for the call."""
     arrs = [_lbfgsb_arrays(x0) for x0 in x0s]
-    chans = [_native.FgChannel(surf, k, max(1, len(g)), cal.spot, cal.risk_free_rate, cal.N)
+    chans = [_native.FgChannel(surf, k, max(1, len(g)), cal.spot, cal.risk_free_rate, cal.N,
+                               ctx=_slot_ctx(surf, k) if len(groups) > 1 else surf.ctx)
              for k, g in enumerate(groups)]
-    with surf.ctx._lock:
-        rc, launches, evals, rows = loop.run(chans[0].loop_device(), [list(g) for g in groups],
+    dev = chans[0].loop_device()
+    dev = dev[:3] + (tuple(ch.ctx.handle.value for ch in chans),) + dev[4:]
+    with contextlib.ExitStack() as stack:
+        for c in {id(ch.ctx): ch.ctx for ch in chans}.values():
+            stack.enter_context(c._lock)
+        rc, launches, evals, rows = loop.run(dev, [list(g) for g in groups],
                                              [ch.loop_slot() for ch in chans], arrs,
                                              _lbfgsb.setulb, np.exp, np.tanh,
                                              _loop_consts(maxiter))

@@ -520,6 +520,36 @@ def test_native_loop_equals_python_loop(dh, calib_golden, monkeypatch, mode):
     assert sa == sb and (la, ea) == (lb, eb)
 
 
+@pytest.mark.parametrize("groups", ["2", "3"])
+def test_pipelined_slots_on_their_own_streams(dh, calib_golden, monkeypatch, groups):
+    """The pipelined loop's slots on contexts of their own (default: Context.slot_context, one
+    stream each, so the groups' requests may overlap on the GPU) and all on the surface's context
+    ($DHCOS_SCIPY_STREAMS=0) give the same calibration bit for bit; the exact-mode setting follows
+    the surface's context onto the slot contexts."""
+    from dhcos import calibrator as CM
+    g = calib_golden
+    x0s = [np.array(s["x0"]) for s in g["calibrate_seed0_starts"]]
+    monkeypatch.setenv("DHCOS_SCIPY_GROUPS", groups)
+    outs = {}
+    for streams in ("1", "0"):
+        monkeypatch.setenv("DHCOS_SCIPY_STREAMS", streams)
+        cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+        outs[streams] = (CM.run_starts(cal, x0s, 300, lockstep=True, pipeline=True),
+                         cal.start_stats, cal.lockstep_launches)
+    (a, sa, la), (b, sb, lb) = outs["1"], outs["0"]
+    for (ra, _), (rb, _) in zip(a, b):
+        assert np.array_equal(ra.x, rb.x) and ra.fun == rb.fun and np.array_equal(ra.jac, rb.jac)
+        assert (ra.nit, ra.nfev, ra.message) == (rb.nit, rb.nfev, rb.message)
+    assert sa == sb and la == lb
+    ctx = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])._get_surface().ctx
+    ctx.set_exact(True)
+    try:
+        assert ctx.slot_context(1)._settings.get("set_exact") is True
+    finally:
+        ctx.set_exact(False)
+        ctx.slot_context(1)
+
+
 def test_fg_begin_end_slots(dh, calib_golden):
     """The asynchronous halves of dh_surface_fg: two requests in flight (one per slot) give
     fg's bits; a busy slot, an empty slot and a bad slot index are errors."""
