@@ -678,7 +678,7 @@ constexpr bool kAheadSkipStage = DH_AHEAD_SKIP_STAGE;   // the writer wave stage
 // The writer: the staging wave before the first barrier (0), or the cut wave during the CF loop,
 // which leaves it idle on C3's tables, right before its ahead_cut (1)
 #ifndef DH_AHEAD_ON_CUT
-#define DH_AHEAD_ON_CUT 0
+#define DH_AHEAD_ON_CUT 1     // 0 (the staging wave, before the first barrier): C3 +0.2%
 #endif
 constexpr bool kAheadOnCut = DH_AHEAD_ON_CUT;
 
