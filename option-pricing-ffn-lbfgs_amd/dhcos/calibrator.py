@@ -548,13 +548,17 @@ def _pipeline_surface(cal, n_starts, force=None):
 
 
 def _pipeline_groups(surf, n_starts):
-    """How many groups (request slots) the pipelined loop splits the starts into: two, or
-    $DHCOS_SCIPY_GROUPS (up to _native.FG_SLOTS).  Measured with the native loop (round 5,
-    calibrate(300, 3)): every start on its own slot is slower than two groups on C1 (4.72 vs
-    4.42 ms) and C2 (6.24 vs 5.94 ms) -- each extra request costs the device more than the host
-    work it hides -- and C3 is device-bound."""
+    """How many groups (request slots, each on its own stream: _slot_ctx) the pipelined loop
+    splits the starts into: one per start (up to _native.FG_SLOTS) when one start's request is a
+    small grid (14 x tiles <= 256 blocks: C1), whose concurrent requests share the GPU; else two
+    (C2, C3: larger requests overlap less and each extra one costs device time).  Measured with the
+    native loop (round 5, calibrate(300, 3), medians of 7): C1 3.98 ms with three against 4.20 ms
+    with two, C2 4.75 / 4.64 ms, C3 8.91 / 8.68 ms.  $DHCOS_SCIPY_GROUPS overrides."""
     env = os.environ.get("DHCOS_SCIPY_GROUPS", "")
-    G = int(env) if env else 2
+    if env:
+        G = int(env)
+    else:
+        G = _native.FG_SLOTS if (N_PARAMS + 1) * max(1, surf.n_tiles) <= 256 else 2
     return max(1, min(G, n_starts, _native.FG_SLOTS))
 
 
