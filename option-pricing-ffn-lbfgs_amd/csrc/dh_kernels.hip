@@ -119,9 +119,10 @@ struct PriceArgs {
                             // term summed); set by launch_price
     // prologues ahead (fused kernel, requests of more than one round of resident blocks): block
     // q < ahead_stride forms the prologue constants of tables q + j ahead_stride (j = 1 ..
-    // kAheadMax) into ahead[.][kAheadRec], tagged with ahead_epoch; a later block whose tag holds
-    // this launch's epoch loads its constants instead of forming them
+    // kAheadMax) into ahead[.][kTabC] and then sets ahead_flag[.] = ahead_epoch; a later block
+    // whose flag holds this launch's epoch loads its constants instead of forming them
     double* ahead;
+    unsigned* ahead_flag;
     int ahead_stride;       // 0: off
     unsigned ahead_epoch;
 };
@@ -651,26 +652,35 @@ __device__ __forceinline__ int cf_cut_group8(const dh::Params& P, double T, doub
 // Prologues ahead (round 5).  A fused request of more than one round of resident blocks (C3:
 // 4,200 tables on 1,024 slots) spends ~18% of every block's chain, and ~1,000 wave-instructions
 // per table, on the serial prologue (table_prologue_wave + the CF-cut test).  Its first-round
-// blocks form the later-round tables' prologues on the cut wave during the CF loop, which leaves
-// that wave idle on C3's tables: 8 lanes per table (the two variance factors on sub-lanes 0 and 1,
-// the six exponentials on sub-lanes 0 .. 5: table_prologue_wave's expressions on the same
+// blocks form the later-round tables' prologues on a wave that otherwise only stages a few
+// options before the first barrier: 8 lanes per table (the two variance factors on sub-lanes 0
+// and 1, the six exponentials on sub-lanes 0 .. 5: table_prologue_wave's expressions on the same
 // operands, uncontracted, so the same bits), the CF-cut candidates 8 at a time (cf_cut_group8:
-// the same first passing candidate as the wave's ballot).  The record goes out with agent-scope
-// stores; once they have drained (s_waitcnt vmcnt(0)) the table's tag takes the launch's epoch
-// and K_cf -- MI355X_MICROARCH.md's "valid forms" row 1, as the loss hand-off.  A later block
-// reads its tag: this launch's, it loads the record (wave 0) and takes K_cf from the tag (the cut
-// wave); not (its writer has not got there: never seen, dispatch runs in block order and a later
-// block starts only after a whole block lifetime), it forms them itself.  Either way the same
-// values, so the same bits.
+// the same first passing candidate as the wave's ballot).  The constants go out with agent-scope
+// stores; after the CF loop (the stores long drained: s_waitcnt vmcnt(0)) a flag per table takes
+// the launch's epoch -- MI355X_MICROARCH.md's "valid forms" row 1, as the loss hand-off.  A
+// later block reads its flag: set, it loads the 31 constants (wave 0 slots 0 .. 29, the cut wave
+// slot 30); not set (its writer has not got there: never seen, dispatch runs in block order and
+// a later block starts only after a whole block lifetime), it forms them itself.  Either way the
+// same values, so the same bits.
 // ----------------------------------------------------------------------------------------------
 constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane groups of a wave
-// What travels per later table, in one 128-byte line ahead[q * kAheadRec ..]: the prologue's
-// values that cost a transcendental or a cumulant chain -- a, b, e^b, e^a, the clamp bounds' slots
-// 25 and 26, e^{-rT}, the CF drift (values 0 .. 7: one coalesced 64-byte store by the writer
-// group's 8 lanes) -- and the tag (value 8, 64 bits: the launch's epoch << 32 | K_cf), stored after
-// the values have drained; the reader re-forms the other slots (2/(b - a), pi/(b - a), the
+// What travels per later table: the prologue's values that cost a transcendental or a cumulant
+// chain -- a, b, e^b, e^a, the clamp bounds' slots 25 and 26, e^{-rT}, the CF drift and K_cf --
+// at ahead[q * kAheadRec + i] (one 128-byte line per table, the writer group's 8 lanes storing 8
+// of them in one coalesced store); the reader re-forms the other slots (2/(b - a), pi/(b - a), the
 // factors' constants, S0, r, T, the group) from the parameters by the same expressions.
 constexpr int kAheadRec = 16;
+#ifndef DH_AHEAD_SKIP_STAGE
+#define DH_AHEAD_SKIP_STAGE 0     // 1 measured slower on C3 (58.5 vs 57.8 us kernel)
+#endif
+constexpr bool kAheadSkipStage = DH_AHEAD_SKIP_STAGE;   // the writer wave stages no options
+// The writer: the staging wave before the first barrier (0), or the cut wave during the CF loop,
+// which leaves it idle on C3's tables, right before its ahead_cut (1)
+#ifndef DH_AHEAD_ON_CUT
+#define DH_AHEAD_ON_CUT 1     // 0 (the staging wave, before the first barrier): C3 +0.2%
+#endif
+constexpr bool kAheadOnCut = DH_AHEAD_ON_CUT;
 
 // v of lane (lane & ~7) | l: the 8-lane group's broadcast
 __device__ __forceinline__ double grp8_bcast(double v, int l) {
@@ -698,9 +708,9 @@ __device__ __forceinline__ int64_t ahead_table(const PriceArgs& A, int64_t q0, i
     return act ? qa : q0;
 }
 
-// The writer (the cut wave of a first-round block, during the CF loop): tables q0 + (j + 1) R,
-// j = lane / 8, values 0 .. 7 of the record into ahead[]; each group's truncation range into ab[j]
-// for ahead_cut, which then forms K_cf and stores the tag
+// The writer (the staging wave, before the first barrier): tables q0 + (j + 1) R, j = lane / 8,
+// values 0 .. 7 of the record into ahead[]; each group's truncation range into ab[j] for the cut
+// wave, which forms value 8 (K_cf) during the CF loop (ahead_cut)
 __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead& H, int64_t q0,
                                             int64_t nblocks, int lane, double (*ab)[2]) {
 #pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
@@ -807,9 +817,9 @@ __device__ __forceinline__ void ahead_read(const PriceArgs& A, const FusedHead& 
     }
 }
 
-// After ahead_write on the same wave: each group's K_cf by cf_cut_group8 on the writer's range
-// (the same first passing candidate as the wave's ballot); then, the record's stores drained,
-// the tag (epoch << 32 | K_cf).
+// The cut wave's part (after its own K_cf, during the CF loop, which leaves it idle up to
+// K_cf = 192): each group's K_cf by cf_cut_group8 on the writer's range (the same first passing
+// candidate as the wave's ballot), into slot 30; then its stores drained.
 __device__ __forceinline__ void ahead_cut(const PriceArgs& A, const FusedHead& H, int64_t q0,
                                           int64_t nblocks, int lane, const double (*ab)[2]) {
     bool act;
@@ -823,23 +833,27 @@ __device__ __forceinline__ void ahead_cut(const PriceArgs& A, const FusedHead& H
                         ? A.N
                         : cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N,
                                         lane & 7);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the record's values drained
-    if (act && (lane & 7) == 0)
-        __hip_atomic_store((unsigned long long*)(A.ahead + q * kAheadRec + 8),
-                           ((unsigned long long)A.ahead_epoch << 32) | (unsigned)kcf,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (act && (lane & 7) == 0) agent_store(A.ahead + q * kAheadRec + 8, kcf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// The reader: table q's tag (a wave-uniform value); this launch's constants are in ahead[] when
-// its high word is the launch's epoch, K_cf in its low word
-__device__ __forceinline__ unsigned long long ahead_tag(const PriceArgs& A, int64_t q) {
-    const unsigned long long w = __hip_atomic_load(
-        (const unsigned long long*)(A.ahead + q * kAheadRec + 8), __ATOMIC_RELAXED,
-        __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)w);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(w >> 32));
-    return ((unsigned long long)hi << 32) | lo;
+// The flags, after both waves' stores drained and a barrier (every lane of a wave calls this)
+__device__ __forceinline__ void ahead_publish(const PriceArgs& A, int64_t q0, int64_t nblocks,
+                                              int lane) {
+    bool act;
+    const int64_t qa = ahead_table(A, q0, nblocks, lane, act);
+    if ((lane & 7) == 0 && act)
+        __hip_atomic_store(&A.ahead_flag[qa], A.ahead_epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// The reader: this launch's constants of table q are in ahead[] (a wave-uniform answer)
+__device__ __forceinline__ bool ahead_ready(const PriceArgs& A, int64_t q) {
+    const unsigned f = __hip_atomic_load(&A.ahead_flag[q], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(f) == A.ahead_epoch;
+}
+
 
 // Every table's prologue of a large fused request ahead of the fused launch (launch_fused): the
 // fused blocks then load their constants instead of running the one-wave prologue chain while
@@ -2088,29 +2102,28 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // (the <= 96-VGPR wide build runs it on wave 0 after the prologue: one range computation
     // less, and the build's register allocation gains: C4 -2.6%)
     const int wcut = (nthr > 64 && WV <= DH_FUSED_WAVES) ? nthr / 64 - 1 : 0;
-    // prologues ahead (4-wave build, >= 3 waves): a first-round block's cut wave writes the
-    // later tables' records; whether this block's constants may have been formed ahead
+    // prologues ahead (4-wave build, >= 3 waves): the first-round block's writer wave, and
+    // whether this block's constants may have been formed ahead
     const int64_t R = (WV <= DH_FUSED_WAVES && nthr >= 192) ? A.ahead_stride : 0;
+    const int wahead = kAheadOnCut ? wcut : nthr / 64 - 2;
     const bool ahead_w = R > 0 && q < R;
     const bool ahead_r = R > 0 && q >= R && q < (kAheadMax + 1) * R;
     const int64_t nblocks = gridDim.x;
-    if (!H.pre && (wv == 0 || wv == wcut)) serial_prio(true);
+    if (!H.pre && (wv == 0 || wv == wcut || (ahead_w && wv == wahead))) serial_prio(true);
     if (H.pre) {
         if (t < kTabC) shc[t] = H.pre[q * kTabC + t];
     } else if (wv == 0) {
-        // (each of the two waves decides on its own tag load and fills its own slots: loaded or
-        // formed, the same values, so a tag set between the two loads changes nothing)
-        const unsigned long long tag = ahead_r ? ahead_tag(A, q) : 0ull;
-        if ((unsigned)(tag >> 32) == A.ahead_epoch && ahead_r) {
+        // (each of the two waves decides on its own flag load and fills its own slots: loaded or
+        // formed, the same values, so a flag set between the two loads changes nothing)
+        if (ahead_r && ahead_ready(A, q)) {
             ahead_read(A, H, q, shc, lane);
-            if (wcut == 0 && lane == 0) shc[30] = (int)(unsigned)tag;
+            if (wcut == 0 && lane == 0) shc[30] = agent_load(A.ahead + q * kAheadRec + 8);
         } else {
             table_prologue_wave(A, H, q, shc, lane, wcut == 0);
         }
     } else if (wv == wcut) {
-        const unsigned long long tag = ahead_r ? ahead_tag(A, q) : 0ull;
-        if ((unsigned)(tag >> 32) == A.ahead_epoch && ahead_r) {
-            if (lane == 0) shc[30] = (int)(unsigned)tag;
+        if (ahead_r && ahead_ready(A, q)) {
+            if (lane == 0) shc[30] = agent_load(A.ahead + q * kAheadRec + 8);
         } else {
             const int kcf = A.N < kCfCutMinN ? A.N : prologue_cut_wave(A, H, q, lane);
             if (lane == 0) shc[30] = kcf;
@@ -2133,8 +2146,13 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const double* prm = H.prm + p * DH_PARAM_STRIDE;
     const double S0 = prm[13];
     dh::load_math_tables(sct, nthr > 64 ? 64 : 0);      // the waves after the prologue's
-    // staging order: waves 1, 2, .., then 0 (its prologue first)
-    for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
+    // staging order: waves 1, 2, .., then 0 (its prologue first); a first-round block's writer
+    // wave stages nothing (its ahead_write chain is the longest before the barrier)
+    const bool ws = ahead_w && kAheadSkipStage;
+    int ts = (t + nthr - 64) % nthr;
+    if (ws && wv > wahead) ts -= 64;
+    if (ws && wv == 0) ts -= 64;
+    for (int i = ts; !(ws && wv == wahead) && i < gn; i += ws ? nthr - 64 : nthr) {
         const int m = g0 + i;
         const double K = option_strike(A, m, S0);
         double ratio;
@@ -2146,6 +2164,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         L.xK[i] = xK;
         L.exK[i] = ratio;
     }
+    if (!kAheadOnCut && ahead_w && wv == wahead) ahead_write(A, H, q, nblocks, lane, ahd_ab);
     __syncthreads();
     serial_prio(false);
     if (__builtin_amdgcn_readfirstlane(live_v) <= 0) return;   // every block reads the same count
@@ -2228,17 +2247,19 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP_T(A, 17, 128);
         DH_STAMP_T(A, 18, 192);
     }
-    // prologues ahead, on the cut wave during the CF loop (on C3's tables K_cf <= 192 leaves it
-    // idle there): the later tables' records, their K_cf, and the tags once the records drained
+    // prologues ahead: the later tables' K_cf on the cut wave; both writer waves' stores drained
+    // before the barrier, the flags after it
     if (ahead_w && wv == wcut) {
-        ahead_write(A, H, q, nblocks, lane, ahd_ab);
+        if (kAheadOnCut) ahead_write(A, H, q, nblocks, lane, ahd_ab);
         ahead_cut(A, H, q, nblocks, lane, ahd_ab);
     }
+    if (ahead_w && wv == wahead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (!kEarlyClamp) clamp_scan();
     DH_STAMP(A, 21);
     DH_STAMP_T(A, 22, 64);
     __syncthreads();
     DH_STAMP(A, 2);
+    if (ahead_w && wv == wahead) ahead_publish(A, q, nblocks, lane);
 
     // ---- k-sums in the canonical order of a 64-thread table slot (from the LDS table; the same
     //      bits as cos_table_kernel).  c1 is a sum of zeros (+0.0) and w0 has one nonzero term
@@ -2604,10 +2625,11 @@ struct dh_ctx {
     int stamps_on = 0;      // diagnostic builds: record per-block phase stamps
     DevBuf stamps;
     int64_t stamps_n = 0;
-    // prologues ahead (launch_fused): the later-round tables' records and tags, the launch
+    // prologues ahead (launch_fused): constants and flags of the later-round tables, the launch
     // epoch, $DHCOS_AHEAD (-1: not read yet; 0 turns it off) and the resident-block counts of the
     // fused kernel builds it applies to, by (t1, r1, LDS bytes)
-    DevBuf ahead;
+    DevBuf ahead, ahead_flag;
+    size_t ahead_flag_cap = 0;
     unsigned ahead_epoch = 0;
     int ahead_on = -1;
     int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
@@ -2786,6 +2808,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     const double* tsrc = A.paired ? A.T : A.group_T;       // FusedHead: preloaded arguments
     const bool r1 = tile_r(max_nopt, t2) == 1;
     A.ahead = nullptr;
+    A.ahead_flag = nullptr;
     A.ahead_stride = 0;
     if (ctx->ahead_on < 0) {
         const char* e = std::getenv("DHCOS_AHEAD");
@@ -2816,12 +2839,15 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
             ctx->resident_fused.push_back({key, res});
         }
         if (blocks > res) {
-            const size_t cap0 = ctx->ahead.cap;
             HIP_TRY(ctx->ahead.reserve((size_t)blocks * kAheadRec * sizeof(double)));
-            if (ctx->ahead.cap != cap0)                            // fresh records: tag 0
-                HIP_TRY(hipMemsetAsync(ctx->ahead.ptr, 0, ctx->ahead.cap, st));
-            if (++ctx->ahead_epoch == 0) ++ctx->ahead_epoch;     // 0: a cleared tag's epoch
+            if ((size_t)blocks > ctx->ahead_flag_cap) {
+                HIP_TRY(ctx->ahead_flag.reserve((size_t)blocks * sizeof(unsigned)));
+                HIP_TRY(hipMemsetAsync(ctx->ahead_flag.ptr, 0, ctx->ahead_flag.cap, st));
+                ctx->ahead_flag_cap = ctx->ahead_flag.cap / sizeof(unsigned);
+            }
+            if (++ctx->ahead_epoch == 0) ++ctx->ahead_epoch;     // 0: the cleared flags' value
             A.ahead = (double*)ctx->ahead.ptr;
+            A.ahead_flag = (unsigned*)ctx->ahead_flag.ptr;
             A.ahead_stride = res;
             A.ahead_epoch = ctx->ahead_epoch;
             // and the loss sums in a launch of their own (loss_partials_kernel)
