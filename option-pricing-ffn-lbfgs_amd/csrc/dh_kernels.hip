@@ -2611,10 +2611,6 @@ struct dh_ctx {
         int S = 0, M = 0;
         const dh_surface* surf = nullptr;   // the surface the request was enqueued on
         bool pending = false;
-        // the request's completion: an event recorded behind it, or (no other slot's request on
-        // the stream) the stream itself going idle -- a later request on the same stream records
-        // this slot's event first (dh_surface_fg_begin)
-        bool evented = false;
         hipEvent_t done = nullptr;
     } fg[DH_FG_SLOTS];
     DevBuf lb_trace, lb_trace_n;   // diagnostic request trace of dh_calibrate_lbfgs
@@ -4551,15 +4547,6 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     bool others = false;
     for (int o = 0; o < DH_FG_SLOTS; ++o) others = others || (o != slot && ctx->fg[o].pending);
     if (others && !covered) HIP_TRY(hipStreamSynchronize(ctx->stream));
-    // a request behind another slot's on this stream: that slot's completion becomes an event now,
-    // while the stream holds only what it waits for
-    for (int o = 0; o < DH_FG_SLOTS; ++o) {
-        auto& O = ctx->fg[o];
-        if (o == slot || !O.pending || O.evented) continue;
-        if (!O.done) HIP_TRY(hipEventCreateWithFlags(&O.done, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(O.done, ctx->stream));
-        O.evented = true;
-    }
     if (s != ctx->fg_surf || N != ctx->fg_N) {
         ctx->fg_surf = s;
         ctx->fg_N = N;
@@ -4576,7 +4563,6 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     F.surf = s;
     if (S == 0) {
         HIP_TRY(hipEventRecord(F.done, ctx->stream));
-        F.evented = true;
         F.pending = true;
         return DH_OK;
     }
@@ -4585,8 +4571,8 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
                              (double*)F.h_loss.dptr, (int32_t*)((double*)F.h_loss.dptr + P),
                              nullptr, ctx->stream);
     if (rc) return rc;
-    F.evented = false;                  // the stream going idle marks it, unless a later request
-    F.pending = true;                   // on this stream records the event first
+    HIP_TRY(hipEventRecord(F.done, ctx->stream));
+    F.pending = true;
     return DH_OK;
 }
 
@@ -4607,12 +4593,11 @@ extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, int
     if (dev_scope.rc) return dev_scope.rc;
     const size_t P = (size_t)F.S * dhlb::kPts;
     for (;;) {                          // busy-wait: an optimizer iteration waits on it
-        const hipError_t e = F.evented ? hipEventQuery(F.done) : hipStreamQuery(ctx->stream);
+        const hipError_t e = hipEventQuery(F.done);
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) {
             F.pending = false;
-            return fail(DH_E_HIP, std::string(F.evented ? "hipEventQuery: " : "hipStreamQuery: ") +
-                                      hipGetErrorString(e));
+            return fail(DH_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
         }
     }
     F.pending = false;
@@ -4629,7 +4614,7 @@ extern "C" int dh_surface_fg_cancel(dh_ctx* ctx, int slot) {
     DeviceScope dev_scope(ctx->device);
     if (dev_scope.rc) return dev_scope.rc;
     F.pending = false;                  // cleared even if the wait fails: the slot is usable again
-    HIP_TRY(F.evented ? hipEventSynchronize(F.done) : hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipEventSynchronize(F.done));
     return DH_OK;
 }
 
