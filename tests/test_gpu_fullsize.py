@@ -151,7 +151,7 @@ def test_c3_objective_and_fd_gradient_match_oracle(dh):
     ratio = p_or / mkt
     B = 2 * eps * np.mean(np.abs(ratio - 1) * ratio, axis=1) + eps ** 2 * np.mean(ratio ** 2, axis=1)
     tol_g = 2 * (2 * B)[:, None] / dx
-    f_s, g_s, _ = cal.fg_batch(x0s)                         # the SciPy driver's first request
+    f_s, g_s, low_s = cal.fg_batch(x0s)                     # the SciPy driver's first request
     surf.ctx.set_lb_trace(64)
     try:
         surf.calibrate_lbfgs(x0s, S0, r, N, maxiter=1)
@@ -167,6 +167,12 @@ def test_c3_objective_and_fd_gradient_match_oracle(dh):
             assert abs(f - f_or[s, 0]) <= 1e-9 * abs(f_or[s, 0]), (s, name)
             assert abs(f - f_or[s, 0]) <= 2 * B[s], (s, name)
             assert np.all(np.abs(g - g_or[s]) <= tol_g[s]), (s, name, g - g_or[s], tol_g[s])
+    # the pipelined driver's asynchronous request (dh_surface_fg_begin / _end: the multi-round
+    # fused launch's partial pairs summed on the host) is fg_batch's synchronous one bit for bit
+    from dhcos.calibrator import fd_models
+    surf.fg_begin(x0s, S0, r, N, model=fd_models(x0s), slot=1)
+    for u, v in zip(surf.fg_end(1), (f_s, g_s, low_s)):
+        assert np.array_equal(u, v)
 
 
 @pytest.mark.parametrize("driver", ["scipy", "device"])
