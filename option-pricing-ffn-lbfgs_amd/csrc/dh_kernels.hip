@@ -2612,9 +2612,6 @@ struct dh_ctx {
         const dh_surface* surf = nullptr;   // the surface the request was enqueued on
         bool pending = false;
         hipEvent_t done = nullptr;
-        HostBuf h_part;            // the fused launch's (partial, invalid count) pairs, [P][n_tiles]
-        bool host_part = false;    // this request's sums are formed here (dh_surface_fg_end)
-        int n_tiles = 0;
     } fg[DH_FG_SLOTS];
     DevBuf lb_trace, lb_trace_n;   // diagnostic request trace of dh_calibrate_lbfgs
     hipEvent_t lb_ev[2] = {nullptr, nullptr};   // chunk-completion events of dh_calibrate_lbfgs
@@ -2635,11 +2632,6 @@ struct dh_ctx {
     size_t ahead_flag_cap = 0;
     unsigned ahead_epoch = 0;
     int ahead_on = -1;
-    // dh_surface_fg_begin's loss launch: the (partial, invalid count) pairs go to this mapped host
-    // buffer when the launch is fused (fg_host_part_used), and dh_surface_fg_end sums them
-    double* fg_host_part = nullptr;
-    bool fg_host_part_used = false;
-    int host_part_on = -1;     // $DHCOS_HOST_PARTIALS (0: off)
     int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
                                // in loss_partials_kernel (-1: not read yet)
     std::vector<std::pair<std::array<int64_t, 3>, int>> resident_fused;
@@ -2825,14 +2817,6 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     // prologues ahead: the 4-wave build of >= 3-wave blocks, more blocks than one round of
     // resident ones, in-block prologues (no prologue kernel)
     const bool wide = r1 && blocks >= kFusedWideMinBlocks;
-    // a host driver's request (dh_surface_fg_begin): every block stores its pair straight into
-    // the slot's mapped buffer and ends -- no hand-off, no summing launch; the host sums them
-    const bool host_part = ctx->fg_host_part && A.part_sse && !A.partials_only && !A.paired;
-    if (host_part) {
-        A.part_sse = ctx->fg_host_part;
-        A.partials_only = 2;
-        ctx->fg_host_part_used = true;
-    }
     if (ctx->ahead_on && !wide && block.x >= 192 && blocks < kPrologueKernelMinBlocks) {
         const std::array<int64_t, 3> key{t1, r1 ? 1 : 0, (int64_t)lds};
         int res = -1;
@@ -2908,7 +2892,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         default: hipLaunchKernelGGL((cos_fused_kernel<256, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
     }
     HIP_TRY(hipGetLastError());
-    if (A.partials_only == 2 && !host_part) {
+    if (A.partials_only == 2) {
         hipLaunchKernelGGL(loss_partials_kernel, dim3((unsigned)A.P), dim3(64), 0, st,
                            (const double2*)A.part_sse, A.n_tiles, A.sse, A.n_bad);
         HIP_TRY(hipGetLastError());
@@ -3129,7 +3113,6 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     for (auto& F : ctx->fg) {
         F.h_params.release();
         F.h_loss.release();
-        F.h_part.release();
         if (F.done) (void)hipEventDestroy(F.done);
     }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -4507,34 +4490,6 @@ void fg_finish(int S, int M, const double* sse, const int32_t* bad, const double
     }
 }
 
-// The sums loss_partials_kernel (and the in-kernel hand-off) form, on the host: per param set,
-// lane l of 64 adds pairs j = l, l + 64, ... in order from +0, then the xor butterfly over offsets
-// 1, 2, .., 32 (xor_sum: every lane ends with the same sum; IEEE addition commutes), so the same
-// bits.  part: [P][n_tiles] (partial, invalid count) pairs.
-void host_partial_sums(const double* part, int P, int n_tiles, double* sse, int32_t* bad) {
-    for (int p = 0; p < P; ++p) {
-        double acc[64], nb[64], ta[64], tb[64];
-        for (int l = 0; l < 64; ++l) acc[l] = nb[l] = 0.0;
-        const double* q = part + (size_t)p * n_tiles * 2;
-        for (int j = 0; j < n_tiles; ++j) {
-            acc[j & 63] += q[2 * j];
-            nb[j & 63] += q[2 * j + 1];
-        }
-        for (int off = 1; off < 64; off <<= 1) {
-            for (int l = 0; l < 64; ++l) {
-                ta[l] = acc[l] + acc[l ^ off];
-                tb[l] = nb[l] + nb[l ^ off];
-            }
-            for (int l = 0; l < 64; ++l) {
-                acc[l] = ta[l];
-                nb[l] = tb[l];
-            }
-        }
-        sse[p] = acc[0];
-        bad[p] = (int32_t)nb[0];
-    }
-}
-
 int fg_check(dh_ctx* ctx, const dh_surface* s, int S) {
     if (!s->has_mkt) return fail(DH_E_ARG, "surface has no market prices");
     if (s->M == 0) return fail(DH_E_ARG, "empty market (the loss is NaN)");
@@ -4612,24 +4567,9 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
         return DH_OK;
     }
     fg_points(x0, model, S, S0, r, (double*)F.h_params.ptr, F.pen.data(), F.dx.data());
-    // the fused launch's pairs straight into the slot's mapped buffer, summed in _end
-    if (ctx->host_part_on < 0) {
-        const char* e = std::getenv("DHCOS_HOST_PARTIALS");
-        ctx->host_part_on = (e && e[0] == '0') ? 0 : 1;
-    }
-    F.host_part = false;
-    F.n_tiles = s->n_tiles;
-    if (ctx->host_part_on) {
-        HIP_TRY(F.h_part.reserve(P * (size_t)s->n_tiles * 2 * sizeof(double)));
-        ctx->fg_host_part = (double*)F.h_part.dptr;
-        ctx->fg_host_part_used = false;
-    }
     rc = dh_surface_loss_dev(ctx, s, (const double*)F.h_params.dptr, (int)P, N, L,
                              (double*)F.h_loss.dptr, (int32_t*)((double*)F.h_loss.dptr + P),
                              nullptr, ctx->stream);
-    F.host_part = ctx->fg_host_part && ctx->fg_host_part_used;
-    ctx->fg_host_part = nullptr;
-    ctx->fg_host_part_used = false;
     if (rc) return rc;
     HIP_TRY(hipEventRecord(F.done, ctx->stream));
     F.pending = true;
@@ -4661,9 +4601,6 @@ extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, int
         }
     }
     F.pending = false;
-    if (F.host_part)
-        host_partial_sums((const double*)F.h_part.ptr, (int)P, F.n_tiles, (double*)F.h_loss.ptr,
-                          (int32_t*)((double*)F.h_loss.ptr + P));
     fg_finish(F.S, F.M, (const double*)F.h_loss.ptr, (const int32_t*)((double*)F.h_loss.ptr + P),
               F.pen.data(), F.dx.data(), f, g, low);
     return DH_OK;

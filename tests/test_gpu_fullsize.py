@@ -167,8 +167,8 @@ def test_c3_objective_and_fd_gradient_match_oracle(dh):
             assert abs(f - f_or[s, 0]) <= 1e-9 * abs(f_or[s, 0]), (s, name)
             assert abs(f - f_or[s, 0]) <= 2 * B[s], (s, name)
             assert np.all(np.abs(g - g_or[s]) <= tol_g[s]), (s, name, g - g_or[s], tol_g[s])
-    # the pipelined driver's asynchronous request (dh_surface_fg_begin / _end: the multi-round
-    # fused launch's partial pairs summed on the host) is fg_batch's synchronous one bit for bit
+    # the pipelined driver's asynchronous request (dh_surface_fg_begin / _end on a slot) is
+    # fg_batch's synchronous one bit for bit
     from dhcos.calibrator import fd_models
     surf.fg_begin(x0s, S0, r, N, model=fd_models(x0s), slot=1)
     for u, v in zip(surf.fg_end(1), (f_s, g_s, low_s)):
