@@ -652,17 +652,17 @@ __device__ __forceinline__ int cf_cut_group8(const dh::Params& P, double T, doub
 // Prologues ahead (round 5).  A fused request of more than one round of resident blocks (C3:
 // 4,200 tables on 1,024 slots) spends ~18% of every block's chain, and ~1,000 wave-instructions
 // per table, on the serial prologue (table_prologue_wave + the CF-cut test).  Its first-round
-// blocks form the later-round tables' prologues on a wave that otherwise only stages a few
-// options before the first barrier: 8 lanes per table (the two variance factors on sub-lanes 0
-// and 1, the six exponentials on sub-lanes 0 .. 5: table_prologue_wave's expressions on the same
+// blocks form the later-round tables' prologues on the cut wave during the CF loop, which leaves
+// that wave idle on C3's tables: 8 lanes per table (the two variance factors on sub-lanes 0 and 1,
+// the six exponentials on sub-lanes 0 .. 5: table_prologue_wave's expressions on the same
 // operands, uncontracted, so the same bits), the CF-cut candidates 8 at a time (cf_cut_group8:
 // the same first passing candidate as the wave's ballot).  The constants go out with agent-scope
-// stores; after the CF loop (the stores long drained: s_waitcnt vmcnt(0)) a flag per table takes
-// the launch's epoch -- MI355X_MICROARCH.md's "valid forms" row 1, as the loss hand-off.  A
-// later block reads its flag: set, it loads the 31 constants (wave 0 slots 0 .. 29, the cut wave
-// slot 30); not set (its writer has not got there: never seen, dispatch runs in block order and
-// a later block starts only after a whole block lifetime), it forms them itself.  Either way the
-// same values, so the same bits.
+// stores; once drained (s_waitcnt vmcnt(0)), after the block's CF barrier a flag per table takes
+// the launch's epoch -- MI355X_MICROARCH.md's "valid forms" row 1, as the loss hand-off.  A later
+// block reads its flag: set, it loads the record (wave 0) and K_cf (the cut wave); not set (its
+// writer has not got there: never seen, dispatch runs in block order and a later block starts only
+// after a whole block lifetime), it forms them itself.  Either way the same values, so the same
+// bits.
 // ----------------------------------------------------------------------------------------------
 constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane groups of a wave
 // What travels per later table: the prologue's values that cost a transcendental or a cumulant
@@ -671,17 +671,6 @@ constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane
 // of them in one coalesced store); the reader re-forms the other slots (2/(b - a), pi/(b - a), the
 // factors' constants, S0, r, T, the group) from the parameters by the same expressions.
 constexpr int kAheadRec = 16;
-#ifndef DH_AHEAD_SKIP_STAGE
-#define DH_AHEAD_SKIP_STAGE 0     // 1 measured slower on C3 (58.5 vs 57.8 us kernel)
-#endif
-constexpr bool kAheadSkipStage = DH_AHEAD_SKIP_STAGE;   // the writer wave stages no options
-// The writer: the staging wave before the first barrier (0), or the cut wave during the CF loop,
-// which leaves it idle on C3's tables, right before its ahead_cut (1)
-#ifndef DH_AHEAD_ON_CUT
-#define DH_AHEAD_ON_CUT 1     // 0 (the staging wave, before the first barrier): C3 +0.2%
-#endif
-constexpr bool kAheadOnCut = DH_AHEAD_ON_CUT;
-
 // v of lane (lane & ~7) | l: the 8-lane group's broadcast
 __device__ __forceinline__ double grp8_bcast(double v, int l) {
     const int src = ((int)__lane_id() & ~7) | l;
@@ -708,11 +697,11 @@ __device__ __forceinline__ int64_t ahead_table(const PriceArgs& A, int64_t q0, i
     return act ? qa : q0;
 }
 
-// The writer (the staging wave, before the first barrier): tables q0 + (j + 1) R, j = lane / 8,
-// values 0 .. 7 of the record into ahead[]; each group's truncation range into ab[j] for the cut
-// wave, which forms value 8 (K_cf) during the CF loop (ahead_cut)
+// The writer (a first-round block's cut wave, during the CF loop, which leaves it idle on C3's
+// tables): tables q0 + (j + 1) R, j = lane / 8, values 0 .. 7 of the record and K_cf (value 8)
+// into ahead[], then its stores drained (the flags follow the block's CF barrier)
 __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead& H, int64_t q0,
-                                            int64_t nblocks, int lane, double (*ab)[2]) {
+                                            int64_t nblocks, int lane) {
 #pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
     const int sub = lane & 7;
     bool act;
@@ -752,10 +741,6 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
     CC.half_sj2 = 0.5 * (P.sj * P.sj);
     CC.muj = P.muj;
     CC.lt = P.lam * T;
-    if (sub == 0) {
-        ab[lane >> 3][0] = a;
-        ab[lane >> 3][1] = b;
-    }
     // record value sub of the group's table: a, b, e^b, e^a, slot 25, slot 26, e^{-rT}, drift.
     // The shuffles run on every lane, outside the selection: a lane shuffle inside a branch would
     // read the branch's inactive lanes (sub-lanes 0 and 1 hold e^b and e^a)
@@ -766,6 +751,13 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
     v = sub == 5 ? e3 * (1.0 - kClampMargin) : v;
     v = sub == 7 ? CC.drift : v;
     if (act) agent_store(A.ahead + qa * kAheadRec + sub, v);
+    // K_cf of the group's table by cf_cut_group8 on the same operands (the same first passing
+    // candidate as the wave's ballot), then every store of the wave drained
+    const int kcf = A.N < kCfCutMinN
+                        ? A.N
+                        : cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, sub);
+    if (act && sub == 0) agent_store(A.ahead + qa * kAheadRec + 8, kcf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // The reader (wave 0 of a later block whose flag is set): the record's values and the slots
@@ -817,27 +809,7 @@ __device__ __forceinline__ void ahead_read(const PriceArgs& A, const FusedHead& 
     }
 }
 
-// The cut wave's part (after its own K_cf, during the CF loop, which leaves it idle up to
-// K_cf = 192): each group's K_cf by cf_cut_group8 on the writer's range (the same first passing
-// candidate as the wave's ballot), into slot 30; then its stores drained.
-__device__ __forceinline__ void ahead_cut(const PriceArgs& A, const FusedHead& H, int64_t q0,
-                                          int64_t nblocks, int lane, const double (*ab)[2]) {
-    bool act;
-    const int64_t q = ahead_table(A, q0, nblocks, lane, act);
-    const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
-    const int g = (int)((unsigned)q % (unsigned)H.tpp);
-    const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
-    const double T = H.tsrc[H.paired ? p : g];
-    const double a = ab[lane >> 3][0], b = ab[lane >> 3][1];
-    const int kcf = A.N < kCfCutMinN
-                        ? A.N
-                        : cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N,
-                                        lane & 7);
-    if (act && (lane & 7) == 0) agent_store(A.ahead + q * kAheadRec + 8, kcf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// The flags, after both waves' stores drained and a barrier (every lane of a wave calls this)
+// The flags, after the writer's stores drained and a barrier (every lane of a wave calls this)
 __device__ __forceinline__ void ahead_publish(const PriceArgs& A, int64_t q0, int64_t nblocks,
                                               int lane) {
     bool act;
@@ -2083,7 +2055,6 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     __shared__ double red[4][1];
     __shared__ double2 sct[dh::kMathTab];
     __shared__ unsigned long long cmask[kTileMax / 64];
-    __shared__ double ahd_ab[kAheadMax][2];            // prologues ahead: later tables' ranges
     const int nthr = blockDim.x;
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -2105,11 +2076,10 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // prologues ahead (4-wave build, >= 3 waves): the first-round block's writer wave, and
     // whether this block's constants may have been formed ahead
     const int64_t R = (WV <= DH_FUSED_WAVES && nthr >= 192) ? A.ahead_stride : 0;
-    const int wahead = kAheadOnCut ? wcut : nthr / 64 - 2;
     const bool ahead_w = R > 0 && q < R;
     const bool ahead_r = R > 0 && q >= R && q < (kAheadMax + 1) * R;
     const int64_t nblocks = gridDim.x;
-    if (!H.pre && (wv == 0 || wv == wcut || (ahead_w && wv == wahead))) serial_prio(true);
+    if (!H.pre && (wv == 0 || wv == wcut)) serial_prio(true);
     if (H.pre) {
         if (t < kTabC) shc[t] = H.pre[q * kTabC + t];
     } else if (wv == 0) {
@@ -2146,13 +2116,8 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const double* prm = H.prm + p * DH_PARAM_STRIDE;
     const double S0 = prm[13];
     dh::load_math_tables(sct, nthr > 64 ? 64 : 0);      // the waves after the prologue's
-    // staging order: waves 1, 2, .., then 0 (its prologue first); a first-round block's writer
-    // wave stages nothing (its ahead_write chain is the longest before the barrier)
-    const bool ws = ahead_w && kAheadSkipStage;
-    int ts = (t + nthr - 64) % nthr;
-    if (ws && wv > wahead) ts -= 64;
-    if (ws && wv == 0) ts -= 64;
-    for (int i = ts; !(ws && wv == wahead) && i < gn; i += ws ? nthr - 64 : nthr) {
+    // staging order: waves 1, 2, .., then 0 (its prologue first)
+    for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
         const int m = g0 + i;
         const double K = option_strike(A, m, S0);
         double ratio;
@@ -2164,7 +2129,6 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         L.xK[i] = xK;
         L.exK[i] = ratio;
     }
-    if (!kAheadOnCut && ahead_w && wv == wahead) ahead_write(A, H, q, nblocks, lane, ahd_ab);
     __syncthreads();
     serial_prio(false);
     if (__builtin_amdgcn_readfirstlane(live_v) <= 0) return;   // every block reads the same count
@@ -2249,17 +2213,13 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     }
     // prologues ahead: the later tables' K_cf on the cut wave; both writer waves' stores drained
     // before the barrier, the flags after it
-    if (ahead_w && wv == wcut) {
-        if (kAheadOnCut) ahead_write(A, H, q, nblocks, lane, ahd_ab);
-        ahead_cut(A, H, q, nblocks, lane, ahd_ab);
-    }
-    if (ahead_w && wv == wahead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ahead_w && wv == wcut) ahead_write(A, H, q, nblocks, lane);
     if constexpr (!kEarlyClamp) clamp_scan();
     DH_STAMP(A, 21);
     DH_STAMP_T(A, 22, 64);
     __syncthreads();
     DH_STAMP(A, 2);
-    if (ahead_w && wv == wahead) ahead_publish(A, q, nblocks, lane);
+    if (ahead_w && wv == wcut) ahead_publish(A, q, nblocks, lane);
 
     // ---- k-sums in the canonical order of a 64-thread table slot (from the LDS table; the same
     //      bits as cos_table_kernel).  c1 is a sum of zeros (+0.0) and w0 has one nonzero term
