@@ -2144,9 +2144,9 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     //      it in the 4-wave build (after it, the scan's LDS reads queue behind the table's stores
     //      on the request's critical path: C2 -1.7%), after it in the 5-wave build (before it,
     //      the register allocation of the <= 96-VGPR build costs C4 3%) ----
-    auto clamp_scan = [&]() {
+    auto clamp_scan = [&](int first, int step) {
         bool any_cl = false;
-        for (int base = wv * 64; base < gn; base += nthr) {
+        for (int base = first; base < gn; base += step) {
             const int o = base + lane;
             bool cl = false;
             if (o < gn) {
@@ -2158,7 +2158,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
             any_cl = any_cl || mask != 0;
         }
         if (__builtin_expect(any_cl, 0))
-        for (int base = wv * 64; base < gn; base += nthr) {
+        for (int base = first; base < gn; base += step) {
             const int o = base + lane;
             bool cl = false;
             if (o < gn) {
@@ -2183,7 +2183,16 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         }
     };
     constexpr bool kEarlyClamp = WV <= DH_FUSED_WAVES;
-    if constexpr (kEarlyClamp) clamp_scan();
+    // the scan by the block's last wave when the CF loop leaves it idle (all the tile's options, so
+    // the waves with CF entries start them at once: C2 -5% of a block), else each wave its own
+    // 64-option chunks; a first-round block's last wave writes the prologues ahead instead
+    const int lastw = nthr / 64 - 1;
+    const bool scan_last = lastw > 0 && !ahead_w && (lastw * 64 >= TPT1 || kcf <= lastw * 64);
+    if constexpr (kEarlyClamp) {
+        if (!scan_last) clamp_scan(wv * 64, nthr);
+        else if (wv == lastw) clamp_scan(0, 64);
+    }
+    DH_STAMP(A, 29);
     // ---- CF loop (threads < TPT1, one entry each up to N = 256): expanded table into LDS.
     //      (A lane pair per entry, one Heston factor each, cut C1 by 5% but cost C2 2%: the CF
     //      phase of a C2 request is issue-bound on the CUs that host two blocks.) ----
@@ -2214,7 +2223,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // prologues ahead: the later tables' K_cf on the cut wave; both writer waves' stores drained
     // before the barrier, the flags after it
     if (ahead_w && wv == wcut) ahead_write(A, H, q, nblocks, lane);
-    if constexpr (!kEarlyClamp) clamp_scan();
+    if constexpr (!kEarlyClamp) clamp_scan(wv * 64, nthr);
     DH_STAMP(A, 21);
     DH_STAMP_T(A, 22, 64);
     __syncthreads();
