@@ -2183,15 +2183,9 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         }
     };
     constexpr bool kEarlyClamp = WV <= DH_FUSED_WAVES;
-    // the scan by the block's last wave when the CF loop leaves it idle (all the tile's options, so
-    // the waves with CF entries start them at once: C2 -5% of a block), else each wave its own
-    // 64-option chunks; a first-round block's last wave writes the prologues ahead instead
-    const int lastw = nthr / 64 - 1;
-    const bool scan_last = lastw > 0 && !ahead_w && (lastw * 64 >= TPT1 || kcf <= lastw * 64);
-    if constexpr (kEarlyClamp) {
-        if (!scan_last) clamp_scan(wv * 64, nthr);
-        else if (wv == lastw) clamp_scan(0, 64);
-    }
+    // (measured and not kept: the scan by the block's last wave when the CF loop leaves it idle,
+    // so that the CF waves start their entries at once: C2 -0.1 us, C3 +0.2 us)
+    if constexpr (kEarlyClamp) clamp_scan(wv * 64, nthr);
     DH_STAMP(A, 29);
     // ---- CF loop (threads < TPT1, one entry each up to N = 256): expanded table into LDS.
     //      (A lane pair per entry, one Heston factor each, cut C1 by 5% but cost C2 2%: the CF
