@@ -38,6 +38,16 @@ def test_library_exports_every_header_symbol():
     assert set(_native.SIGNATURES) == set(header_functions())
 
 
+def test_header_constants_match_the_binding():
+    """The Python binding's copies of the header's sizes: the request slots of dh_surface_fg_begin
+    (DH_FG_SLOTS) and the sharded draw's state words (DH_GEN_LOC_WORDS)."""
+    from dhcos import _native
+    txt = open(HEADER).read()
+    consts = dict((k, int(v)) for k, v in re.findall(r"#define (DH_[A-Z_]+) (\d+)", txt))
+    assert consts["DH_FG_SLOTS"] == _native.FG_SLOTS
+    assert consts["DH_GEN_LOC_WORDS"] == _native.GEN_LOC_WORDS
+
+
 def test_library_is_gfx950_code_object():
     """The fat binary carries a gfx950 (MI355X) code object and nothing else."""
     from dhcos import _native
