@@ -3,15 +3,16 @@
 --output-format csv of `python bench.py --no-cpu --no-calib --steps K --warmup W`).
 
 bench.py issues, on one stream and in this order, for the configured request shape:
-  1 correctness-check request (device path), 1 host-API request (the same kernels), W warm-up
-  requests, K timed requests, then host-API and HIP-event-timed requests.
+  1 correctness-check request (device path), max(5, min(K, 50)) host-API requests (the same
+  kernels), the pre-warm's requests (round 5: the line's prewarm.requests), W warm-up requests,
+  K timed requests, then HIP-event-timed requests and the side legs.
 Every one of them is a request-shaped dispatch (the same kernel(s) and grid).  This script picks
 the request-shaped dispatches (the most frequent (kernel, grid) of the COS kernels), takes the
-K timed ones (positions W + 2 .. W + K + 1 among the requests; a request of several kernels is
-counted once per its first kernel) and reports their mean / median device duration and the wall
+K timed ones (after the requests above, --bench reads the pre-warm's count from the line; a
+request of several kernels is counted once per its first kernel) and reports their mean / median device duration and the wall
 span of the timed window per request -- the number comparable to bench.py's ms_per_step.
 
-usage: python tools/request_trace.py TRACE.csv --steps K --warmup W [--out JSON]
+usage: python tools/request_trace.py TRACE.csv --steps K --warmup W [--bench LINE.json] [--out JSON]
 """
 import argparse
 import collections
@@ -25,8 +26,14 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, required=True)
     ap.add_argument("--warmup", type=int, required=True)
+    ap.add_argument("--bench", help="the run's JSON line (its prewarm.requests)")
     ap.add_argument("--out")
     a = ap.parse_args()
+    n_pre = 0
+    if a.bench:
+        with open(a.bench) as fh:
+            line = json.loads(fh.read().strip().splitlines()[-1])
+        n_pre = int(line.get("prewarm", {}).get("requests", 0))
     rows = []
     with open(a.trace) as fh:
         for r in csv.DictReader(fh):
@@ -51,7 +58,8 @@ def main():
         elif cur is not None:
             cur[1] = e
             cur[2] += e - s
-    lo, hi = a.warmup + 2, a.warmup + 2 + a.steps
+    lo = 1 + max(5, min(a.steps, 50)) + n_pre + a.warmup
+    hi = lo + a.steps
     timed = reqs[lo:hi]
     durs = [t[2] / 1e3 for t in timed]          # device time of the request's kernels, us
     span = (timed[-1][1] - timed[0][0]) / 1e3 / len(timed)
