@@ -18,6 +18,7 @@ import argparse
 import collections
 import csv
 import json
+import re
 import statistics
 
 
@@ -27,6 +28,8 @@ def main():
     ap.add_argument("--steps", type=int, required=True)
     ap.add_argument("--warmup", type=int, required=True)
     ap.add_argument("--bench", help="the run's JSON line (its prewarm.requests)")
+    ap.add_argument("--grid", type=int, help="the request's grid (threads); default: the most "
+                    "frequent COS dispatch shape")
     ap.add_argument("--out")
     a = ap.parse_args()
     n_pre = 0
@@ -39,10 +42,14 @@ def main():
         for r in csv.DictReader(fh):
             if "cos_" not in r["Kernel_Name"] and "table_prologue" not in r["Kernel_Name"]:
                 continue
-            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"].split("(")[0],
+            m = re.search(r"(\w+)(?:<[^>]*>)?\(", r["Kernel_Name"])
+            name = m.group(1) if m else r["Kernel_Name"]
+            rows.append((int(r["Dispatch_Id"]), name,
                          int(r["Grid_Size_X"]), int(r["Start_Timestamp"]),
                          int(r["End_Timestamp"])))
     rows.sort()
+    if a.grid:
+        rows = [r for r in rows if r[2] == a.grid]
     shape = collections.Counter((k, g) for _, k, g, _, _ in rows).most_common()
     # a request = one dispatch of each kernel of the dominant shape(s) with the same count
     top = shape[0][1]
