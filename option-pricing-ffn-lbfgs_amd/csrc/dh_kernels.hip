@@ -891,41 +891,6 @@ __device__ __forceinline__ void table_entries(const dh::CfConsts& CC, int t, int
     }
 }
 
-// The fused kernel's CF entries: as table_entries, except on a wave whose one pass holds at most
-// 32 entries (C3's last CF wave: K_cf ~ 143 leaves it 15), where lane j < 32 evaluates entry j's
-// first Heston factor and lane j + 32 its second at once (factor_x on the same operands), the
-// second comes over by permlane32_swap, and lane j adds the jump part and forms the entry
-// (cf_phase_from: the same sum in the same order, so the same bits) -- ~310 instead of ~490 VALU
-// for that wave.  Every lane of the wave runs the factor step (the swap needs them all).
-#ifndef DH_CF_LANE_PAIRS
-#define DH_CF_LANE_PAIRS 1
-#endif
-template <int TPT, typename F>
-__device__ __forceinline__ void table_entries_fused(const dh::CfConsts& CC, int t, int N,
-                                                    double piba, double T, double a, double scale,
-                                                    const double2* sct, F&& emit) {
-    const int rem = N - (t & ~63);                       // this wave's entries in one pass
-    if (DH_CF_LANE_PAIRS && N <= TPT && rem > 0 && rem <= 32) {
-        const int lane = t & 63;
-        const int k = (t & ~63) + (lane & 31);
-        const double u = k * piba;                       // k pi / (b - a)
-        const bool two = lane >= 32;
-        dh::FactorC Fc;
-        {
-            const double* f1 = (const double*)&CC.f1;
-            const double* f2 = (const double*)&CC.f2;
-            double* fc = (double*)&Fc;
-            for (int i = 0; i < (int)(sizeof(dh::FactorC) / 8); ++i) fc[i] = two ? f2[i] : f1[i];
-        }
-        const dh::cplx X = dh::factor_x(Fc, u, T, sct);
-        const dh::cplx X2 = {xor_partner<true>(X.re), xor_partner<true>(X.im)};
-        if (!two && lane < rem)
-            emit(k, u, dh::cf_phase_from(CC, u, a, X, X2, dh::jump_x(CC, u, sct), sct) * scale);
-        return;
-    }
-    table_entries<TPT>(CC, t, N, piba, T, a, scale, sct, emit);
-}
-
 // Grid: a fixed number of blocks (resident capacity), each owning a contiguous range of tables.
 // Tables are taken in batches of up to kBatch: lane i of wave 0 computes the truncation range and
 // CF constants of table i of the batch (one prologue latency for up to 64 tables), then every
@@ -2236,7 +2201,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP(A, 6);
         DH_STAMP_T(A, 19, 64);
         DH_STAMP_T(A, 20, 192);
-        table_entries_fused<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
+        table_entries<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
             if (k == 0) {
                 w0s = 0.5 * w;
                 L.t26[0] = make_double2(0.0, 0.0);
