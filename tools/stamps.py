@@ -9,6 +9,7 @@ s_memtime is per XCD, so only
 differences inside one block are meaningful; read shares, not absolute lengths.
 """
 import argparse
+import collections
 import os
 import sys
 
@@ -98,6 +99,27 @@ def main():
                 sh = [np.mean(simd[:, w] == k) for k in range(4)]
                 print(f"    wave {w}: " + "  ".join(f"{x:.2f}" for x in sh))
             print(f"  waves of a block on one CU: {np.mean((cu == cu[:, :1]).all(axis=1)):.3f}")
+            # co-resident blocks: the same XCD (block id mod 8, round-robin dispatch), shader
+            # engine / array and CU; their block-id differences and whether their waves share SIMDs
+            se = (hw[:, 0] >> 13) & 3
+            sh = (hw[:, 0] >> 12) & 1
+            key = (np.arange(len(st)) % 8) * 10000 + se * 1000 + sh * 100 + cu[:, 0]
+            groups = collections.defaultdict(list)
+            for b, k in enumerate(key):
+                groups[int(k)].append(b)
+            sizes = collections.Counter(len(v) for v in groups.values())
+            diffs = collections.Counter()
+            rot = collections.Counter()
+            same = []
+            for v in groups.values():
+                if len(v) == 2:
+                    diffs[v[1] - v[0]] += 1
+                    same.append(np.mean(simd[v[0]] == simd[v[1]]))
+                    rot[int((simd[v[1], 0] - simd[v[0], 0]) % 4)] += 1
+            print(f"  blocks per CU: {dict(sorted(sizes.items()))}; id differences of CU pairs "
+                  f"(most common): {diffs.most_common(4)}; pairs' waves on the same SIMD: "
+                  f"{np.mean(same) if same else float('nan'):.2f}; SIMD offset of the later block's "
+                  f"wave 0: {dict(sorted(rot.items()))}")
             life = st[:, 5] - st[:, 0]
             ng = surf.n_groups if hasattr(surf, "n_groups") else cfg["nT"]
             g = np.arange(len(st)) % ng
