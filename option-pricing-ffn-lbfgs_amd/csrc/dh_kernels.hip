@@ -2620,7 +2620,7 @@ struct dh_ctx {
     size_t ahead_flag_cap = 0;
     unsigned ahead_epoch = 0;
     int ahead_on = -1;
-    int spread_on = -1;        // $DHCOS_SPREAD (1: on): SIMD-aware CF waves (PriceArgs::spread_ncu)
+    int spread_on = -1;        // $DHCOS_SPREAD (0: off): SIMD-aware CF waves (PriceArgs::spread_ncu)
     int n_cus = 0;
     int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
                                // in loss_partials_kernel (-1: not read yet)
@@ -2803,7 +2803,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     A.spread_ncu = 0;
     if (ctx->spread_on < 0) {
         const char* e = std::getenv("DHCOS_SPREAD");
-        ctx->spread_on = (e && e[0] == '1') ? 1 : 0;
+        ctx->spread_on = (e && e[0] == '0') ? 0 : 1;
         HIP_TRY(hipDeviceGetAttribute(&ctx->n_cus, hipDeviceAttributeMultiprocessorCount,
                                       ctx->device));
     }
