@@ -124,9 +124,6 @@ struct PriceArgs {
     double* ahead;
     unsigned* ahead_flag;
     int ahead_stride;       // 0: off
-    // single-round fused grids of one to two blocks per CU (C2): the CU count; a block whose id
-    // lies in an odd multiple of it runs its CF entries on the waves two SIMDs further (0: off)
-    int spread_ncu;
     unsigned ahead_epoch;
 };
 
@@ -667,7 +664,6 @@ __device__ __forceinline__ int cf_cut_group8(const dh::Params& P, double T, doub
 // after a whole block lifetime), it forms them itself.  Either way the same values, so the same
 // bits.
 // ----------------------------------------------------------------------------------------------
-constexpr int kMaxWaves = 16;      // waves of a 1,024-thread block
 constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane groups of a wave
 // What travels per later table: the prologue's values that cost a transcendental or a cumulant
 // chain -- a, b, e^b, e^a, the clamp bounds' slots 25 and 26, e^{-rT}, the CF drift and K_cf --
@@ -2120,13 +2116,6 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const double* prm = H.prm + p * DH_PARAM_STRIDE;
     const double S0 = prm[13];
     dh::load_math_tables(sct, nthr > 64 ? 64 : 0);      // the waves after the prologue's
-    // the SIMD each wave runs on, for the CF wave assignment below (HW_ID bits 5:4)
-    __shared__ int wsimd[kMaxWaves];
-    if (A.spread_ncu && lane == 0) {
-        unsigned hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        wsimd[wv] = (int)((hw >> 4) & 3u);
-    }
     // staging order: waves 1, 2, .., then 0 (its prologue first)
     for (int i = (t + nthr - 64) % nthr; i < gn; i += nthr) {
         const int m = g0 + i;
@@ -2203,20 +2192,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     //      (A lane pair per entry, one Heston factor each, cut C1 by 5% but cost C2 2%: the CF
     //      phase of a C2 request is issue-bound on the CUs that host two blocks.) ----
     __shared__ double w0s;
-    // CF thread index: t, or (spread) this wave's rank among the block's waves by SIMD, rotated by
-    // two SIMDs on every second block of a CU (co-resident blocks b, b + #CU): the two blocks' CF
-    // waves land on different SIMDs whatever SIMD their waves start on.  Any thread may compute
-    // any entry (the same function of k), so the same bits.
-    int tcf = t;
-    if (A.spread_ncu) {
-        const int rot = ((int)(q / A.spread_ncu) & 1) * 2;
-        auto key = [&](int w) { return (((wsimd[w] - rot) & 3) << 4) | w; };
-        const int mine = key(wv);
-        int rank = 0;
-        for (int w = 0; w < nthr / 64; ++w) rank += key(w) < mine ? 1 : 0;
-        tcf = rank * 64 + lane;
-    }
-    if (tcf < TPT1) {
+    if (t < TPT1) {
         dh::CfConsts CC;
         {
             double* cc = (double*)&CC;
@@ -2225,7 +2201,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         DH_STAMP(A, 6);
         DH_STAMP_T(A, 19, 64);
         DH_STAMP_T(A, 20, 192);
-        table_entries<TPT1>(CC, tcf, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
+        table_entries<TPT1>(CC, t, kcf, piba, T, a, scale, sct, [&](int k, double u, double w) {
             if (k == 0) {
                 w0s = 0.5 * w;
                 L.t26[0] = make_double2(0.0, 0.0);
@@ -2620,8 +2596,6 @@ struct dh_ctx {
     size_t ahead_flag_cap = 0;
     unsigned ahead_epoch = 0;
     int ahead_on = -1;
-    int spread_on = -1;        // $DHCOS_SPREAD (0: off): SIMD-aware CF waves (PriceArgs::spread_ncu)
-    int n_cus = 0;
     int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
                                // in loss_partials_kernel (-1: not read yet)
     std::vector<std::pair<std::array<int64_t, 3>, int>> resident_fused;
@@ -2800,13 +2774,6 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     A.ahead = nullptr;
     A.ahead_flag = nullptr;
     A.ahead_stride = 0;
-    A.spread_ncu = 0;
-    if (ctx->spread_on < 0) {
-        const char* e = std::getenv("DHCOS_SPREAD");
-        ctx->spread_on = (e && e[0] == '0') ? 0 : 1;
-        HIP_TRY(hipDeviceGetAttribute(&ctx->n_cus, hipDeviceAttributeMultiprocessorCount,
-                                      ctx->device));
-    }
     if (ctx->ahead_on < 0) {
         const char* e = std::getenv("DHCOS_AHEAD");
         ctx->ahead_on = (e && e[0] == '0') ? 0 : 1;
@@ -2814,10 +2781,6 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     // prologues ahead: the 4-wave build of >= 3-wave blocks, more blocks than one round of
     // resident ones, in-block prologues (no prologue kernel)
     const bool wide = r1 && blocks >= kFusedWideMinBlocks;
-    // single-round grids of one to two blocks per CU (the 4-wave build)
-    if (ctx->spread_on && !wide && block.x >= 192 && ctx->n_cus > 0 && blocks > ctx->n_cus &&
-        blocks <= 2 * (int64_t)ctx->n_cus)
-        A.spread_ncu = ctx->n_cus;
     if (ctx->ahead_on && !wide && block.x >= 192 && blocks < kPrologueKernelMinBlocks) {
         const std::array<int64_t, 3> key{t1, r1 ? 1 : 0, (int64_t)lds};
         int res = -1;
