@@ -627,6 +627,20 @@ def c2_single_start_leg(world, rank, dev, coll, stream, no_calib=False):
     return out
 
 
+def c1_calibration_leg(world, coll):
+    """configs[0], the reference's own CPU-runnable case: calibrate(300, 3) of the 15-option
+    grid on both optimizer drivers, and the SciPy driver's time over the device driver's (the
+    host-bound driver's gap on the smallest surface, where the per-request round trip is all
+    there is)."""
+    cfg = CONFIGS["c1"]
+    opts, S0, r = make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
+    out = {"workload": "configs[0]: " + cfg["workload"]}
+    for drv in ("scipy", "device"):
+        out[drv] = calib_leg(S0, r, opts, cfg["N"], 3, world, coll, drv, reps=7)
+    out["scipy_over_device"] = out["scipy"]["seconds"] / out["device"]["seconds"]
+    return out
+
+
 def c5_leg(dev, stream, rank):
     """The metric's own N = 128: the generator batch (1M param sets x 32 options)."""
     cfg = CONFIGS["c5"]
@@ -729,8 +743,14 @@ def main():
     _native.default_context().set_path({"auto": _native.PATH_AUTO, "split": _native.PATH_SPLIT,
                                         "fused": _native.PATH_FUSED}[args.path])
     _native.default_context().set_tail_cut(args.tail_cut == "on")
-    # a dedicated (non-null) stream: libdhcos launches on it and the HIP events time it
-    stream = torch.cuda.Stream(device=dev)
+    # a dedicated (non-null) stream: libdhcos launches on it and the HIP events time it.  By
+    # default the context's own stream (wrapped, not created: a torch.cuda.Stream() builds
+    # torch's whole stream pool, dozens of HIP streams over the process's 4 hardware queues, and
+    # the calibration legs measured 4-8% slower next to it; DHCOS_BENCH_STREAM=torch: that)
+    if os.environ.get("DHCOS_BENCH_STREAM", "ctx") == "torch":
+        stream = torch.cuda.Stream(device=dev)
+    else:
+        stream = torch.cuda.ExternalStream(_native.default_context().stream, device=dev)
     torch.cuda.set_stream(stream)
     assert stream.cuda_stream, "expected a non-default HIP stream"
     if cfg.get("gen"):
@@ -752,6 +772,8 @@ def main():
         side["c2_single_start"] = c2_single_start_leg(world, rank, dev, coll, stream,
                                                       args.no_calib)
         side["c5_generator_n128"] = c5_leg(dev, stream, rank)
+        if not args.no_calib:
+            side["c1_calibration"] = c1_calibration_leg(world, coll)
 
     # ---- calibrations/sec: one full calibration of the same surface; at N > 1 its starts are
     # sharded over the ranks (dhcos.distributed; the config's starts per GPU, weak scaling; c4:

@@ -80,6 +80,22 @@ struct Loop {
     double h, sqrt_eps;
 };
 
+// host-time split of the loop (ns; read and cleared by stats()): setulb calls, fd_models,
+// request begin, request end (its wait included), loops
+enum { kTSetulb, kTModels, kTBegin, kTEnd, kTCount };
+long long g_t[kTCount + 1] = {};
+inline long long now_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (long long)ts.tv_sec * 1000000000LL + ts.tv_nsec;
+}
+struct Tick {
+    int b;
+    long long t0 = now_ns();
+    explicit Tick(int bucket) : b(bucket) {}
+    ~Tick() { g_t[b] += now_ns() - t0; }
+};
+
 double wall_time() {                         // time.time()
     timespec ts;
     clock_gettime(CLOCK_REALTIME, &ts);
@@ -99,7 +115,11 @@ int advance(Start& s, const Loop& L) {
                                       s.arr[7], s.arr[8], s.arr[9], L.maxls, s.arr[10]);
         Py_DECREF(f);
         if (!args) return -2;
-        PyObject* r = PyObject_Call(L.setulb, args, nullptr);
+        PyObject* r;
+        {
+            Tick tk(kTSetulb);
+            r = PyObject_Call(L.setulb, args, nullptr);
+        }
         Py_DECREF(args);
         if (!r) {
             if (PyErr_ExceptionMatches(PyExc_Exception)) {
@@ -160,6 +180,7 @@ struct Slot {
 
 // fd_models (dhcos/calibrator.py): model [2][S][13] of the slot's x rows and of x + h
 int fd_models(Slot& sl, int S, const Loop& L) {
+    Tick tk(kTModels);
     double* P = sl.model;
     for (int j = 0; j < S; ++j) {
         const double* x = sl.x + (size_t)j * kN;
@@ -211,6 +232,7 @@ struct Device {
 
 // 0 ok, > 0 a libdhcos error code, -1 a Python exception
 int dev_begin(Device& D, Slot& sl, int k, int S) {
+    Tick tk(kTBegin);
     if (D.begin_cb) {
         PyObject* r = PyObject_CallFunction(D.begin_cb, "ii", k, S);
         if (!r) return -1;
@@ -225,6 +247,7 @@ int dev_begin(Device& D, Slot& sl, int k, int S) {
 }
 
 int dev_end(Device& D, Slot& sl, int k, int S) {
+    Tick tk(kTEnd);
     if (D.end_cb) {
         PyObject* r = PyObject_CallFunction(D.end_cb, "ii", k, S);
         if (!r) return -1;
@@ -427,6 +450,7 @@ PyObject* run(PyObject*, PyObject* args) {
         return true;
     };
 
+    const long long t_run = now_ns();
     bool ok = true;
     for (int k = 0; k < G && ok; ++k) ok = submit(k);
     while (ok) {
@@ -452,6 +476,7 @@ PyObject* run(PyObject*, PyObject* args) {
         }
         if (!any) break;
     }
+    g_t[kTCount] += now_ns() - t_run;
     if (!ok) {
         PyObject *et = nullptr, *ev = nullptr, *tb = nullptr;
         if (py_err) PyErr_Fetch(&et, &ev, &tb);
@@ -482,7 +507,16 @@ PyObject* run(PyObject*, PyObject* args) {
     return Py_BuildValue("(illN)", rc, launches, loss_evals, out);
 }
 
+// stats() -> (setulb, fd_models, begin, end, loop) host ns summed over the runs since the last
+// call (a diagnostic: tools/calib_profile.py)
+PyObject* stats(PyObject*, PyObject*) {
+    PyObject* r = Py_BuildValue("(LLLLL)", g_t[0], g_t[1], g_t[2], g_t[3], g_t[4]);
+    std::memset(g_t, 0, sizeof(g_t));
+    return r;
+}
+
 PyMethodDef kMethods[] = {
+    {"stats", stats, METH_NOARGS, "stats(): the loop's host-time split since the last call"},
     {"run", run, METH_VARARGS,
      "run(device, groups, slots, starts, setulb, exp, tanh, consts): the SciPy driver's request "
      "loop (see dh_scipy_loop.cpp)"},
