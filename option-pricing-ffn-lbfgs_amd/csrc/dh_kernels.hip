@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <cstring>
 #include <numeric>
+#include <type_traits>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -530,6 +531,29 @@ struct FusedKargs {         // cos_fused_kernel's argument list as a struct (its
     PriceArgs A;
 };
 static_assert(offsetof(FusedKargs, A) == kFusedArgsKernargOff, "PriceArgs kernarg offset");
+
+// Small requests' param records in the kernel arguments (cos_fused_kernel<..., KP = true>): the
+// host driver's function+gradient requests of one start (14 records) travel in the
+// launch's kernel-argument segment, which the runtime writes to device memory ahead of the
+// dispatch, instead of being read by the blocks from mapped host memory across PCIe at the start
+// of the request's critical path (C1: 11.9 -> 10.1 us per kernel with the records in HBM).  One
+// start's 14 records: 1,792 bytes, 2,416 with the rest of the arguments and 2,672 with the
+// runtime's hidden ones (28 records would pass the 4 KiB segment).
+constexpr int kKargSets = 14;
+struct KargParams {
+    double v[kKargSets * DH_PARAM_STRIDE];
+};
+struct NoKargParams {
+    int unused;
+};
+struct FusedKargsKP {       // cos_fused_kernel<..., true>'s argument list
+    FusedKargs head;
+    int tpt2;
+    KargParams pb;
+};
+constexpr int kFusedParamsKernargOff = 368;
+static_assert(offsetof(FusedKargsKP, pb) == kFusedParamsKernargOff, "param block kernarg offset");
+static_assert(sizeof(FusedKargsKP) + 256 <= 4096, "kernel arguments over 4 KiB");
 
 // the live count read by launches without one (FusedHead::live): the halt test is then a load
 // like any other, with no branch on the pointer (a branch made the compiler wait for it at the
@@ -2038,12 +2062,15 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
 // the same order and with the same lane partition as cos_table_kernel<TPT1> followed by
 // cos_option_kernel<tpt2>, so the two paths give the same bits.
 // ----------------------------------------------------------------------------------------------
-template <int TPT1, int RT, int WV = DH_FUSED_WAVES>
+template <int TPT1, int RT, int WV = DH_FUSED_WAVES, bool KP = false>
 __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const double* __restrict__ h_prm, const double* __restrict__ h_tsrc,
     const int2* __restrict__ h_groups, const int* __restrict__ h_live,
-    const double* __restrict__ h_pre, int h_tpp, int h_paired, PriceArgs A_, int tpt2) {
-    const FusedHead H{h_prm, h_tsrc, h_groups, h_live ? h_live : &kLiveOne, h_pre, h_tpp,
+    const double* __restrict__ h_pre, int h_tpp, int h_paired, PriceArgs A_, int tpt2,
+    typename std::conditional<KP, KargParams, NoKargParams>::type pb_) {
+    // KP: the records are the param block at the end of the kernel arguments (read in place)
+    const double* prm0 = KP ? karg_ref<KargParams, kFusedParamsKernargOff>().v : h_prm;
+    const FusedHead H{prm0, h_tsrc, h_groups, h_live ? h_live : &kLiveOne, h_pre, h_tpp,
                       h_paired};
     const PriceArgs& A = karg_ref<PriceArgs, kFusedArgsKernargOff>();
     // the halt test's load is issued here (a global load: a flat one would also hold up every
@@ -2596,6 +2623,12 @@ struct dh_ctx {
     size_t ahead_flag_cap = 0;
     unsigned ahead_epoch = 0;
     int ahead_on = -1;
+    // the host copy of the next fused launch's param records (dh_surface_fg_begin sets it
+    // around its launch): fused launches of <= kKargSets records pass them in their kernel
+    // arguments; $DHCOS_KARG_PARAMS=0 turns that off (kp_on: -1 not read yet)
+    const double* kp_src = nullptr;
+    int64_t kp_n = 0;
+    int kp_on = -1;
     int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
                                // in loss_partials_kernel (-1: not read yet)
     std::vector<std::pair<std::array<int64_t, 3>, int>> resident_fused;
@@ -2677,7 +2710,10 @@ int ensure_attrs(dh_ctx* ctx) {
           (const void*)cos_fused_kernel<128, kR>, (const void*)cos_fused_kernel<256, kR>,
           (const void*)cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>,
           (const void*)cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>,
-          (const void*)cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>})
+          (const void*)cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>,
+          (const void*)cos_fused_kernel<64, 1, DH_FUSED_WAVES, true>,
+          (const void*)cos_fused_kernel<128, 1, DH_FUSED_WAVES, true>,
+          (const void*)cos_fused_kernel<256, 1, DH_FUSED_WAVES, true>})
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn));
     // table-kernel grid = resident capacity (each block then owns a contiguous table range)
     int cus = 0;
@@ -2835,25 +2871,43 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
                            dim3(kBlock), 0, st, A, blocks, (double*)ctx->pre.ptr);
         HIP_TRY(hipGetLastError());
     }
+    // small requests whose records were handed over from the host (dh_surface_fg_begin): the
+    // records in the kernel arguments, one-round in-block-prologue launches only
+    if (ctx->kp_on < 0) {
+        const char* e = std::getenv("DHCOS_KARG_PARAMS");
+        ctx->kp_on = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (ctx->kp_on && ctx->kp_src && A.P == ctx->kp_n && A.P <= kKargSets && r1 && !wide &&
+        !A.ahead && blocks < kPrologueKernelMinBlocks && !ctx->stamps_on && !A.exact) {
+        KargParams pb{};
+        std::memcpy(pb.v, ctx->kp_src, (size_t)A.P * DH_PARAM_STRIDE * sizeof(double));
+        switch (t1) {
+            case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
+            case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
+            default: hipLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
+        }
+        HIP_TRY(hipGetLastError());
+        return DH_OK;
+    }
     // grids of many small blocks (C4: 28,672) gain from a fifth wave per SIMD to overlap the
     // blocks' latency-bound phases; small grids keep the 4-wave build, whose blocks are shorter
     // (same arithmetic: only the register allocation differs, so the same bits)
     if (r1 && blocks >= kFusedWideMinBlocks) {
         switch (t1) {
-            case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
-            case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
-            default: hipLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+            case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
+            case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
+            default: hipLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES_WIDE>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
         }
         HIP_TRY(hipGetLastError());
         return DH_OK;
     }
     switch (t1 * (r1 ? 1 : -1)) {
-        case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
-        case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
-        case 256: hipLaunchKernelGGL((cos_fused_kernel<256, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
-        case -64: hipLaunchKernelGGL((cos_fused_kernel<64, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
-        case -128: hipLaunchKernelGGL((cos_fused_kernel<128, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
-        default: hipLaunchKernelGGL((cos_fused_kernel<256, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2); break;
+        case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
+        case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
+        case 256: hipLaunchKernelGGL((cos_fused_kernel<256, 1>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
+        case -64: hipLaunchKernelGGL((cos_fused_kernel<64, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
+        case -128: hipLaunchKernelGGL((cos_fused_kernel<128, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
+        default: hipLaunchKernelGGL((cos_fused_kernel<256, kR>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, NoKargParams{}); break;
     }
     HIP_TRY(hipGetLastError());
     if (A.partials_only == 2) {
@@ -4531,9 +4585,14 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
         return DH_OK;
     }
     fg_points(x0, model, S, S0, r, (double*)F.h_params.ptr, F.pen.data(), F.dx.data());
+    // the records also travel in the fused launch's kernel arguments when they fit (KargParams)
+    ctx->kp_src = (const double*)F.h_params.ptr;
+    ctx->kp_n = (int64_t)P;
     rc = dh_surface_loss_dev(ctx, s, (const double*)F.h_params.dptr, (int)P, N, L,
                              (double*)F.h_loss.dptr, (int32_t*)((double*)F.h_loss.dptr + P),
                              nullptr, ctx->stream);
+    ctx->kp_src = nullptr;
+    ctx->kp_n = 0;
     if (rc) return rc;
     HIP_TRY(hipEventRecord(F.done, ctx->stream));
     F.pending = true;

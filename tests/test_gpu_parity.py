@@ -576,6 +576,28 @@ def test_fg_begin_end_slots(dh, calib_golden):
             assert np.array_equal(u, v)
 
 
+@pytest.mark.parametrize("N", [64, 128, 256])
+def test_fg_begin_single_start_records_in_kernel_arguments(dh, calib_golden, N):
+    """A one-start asynchronous request (14 records) passes its records in the fused launch's
+    kernel arguments (KargParams) instead of mapped host memory; fg's synchronous request reads
+    them from memory.  Same bits, at each fused block width (N = 64 / 128 / 256), and a
+    two-start request (28 records, from memory) alongside in another slot."""
+    from dhcos.calibrator import fd_models
+    g = calib_golden
+    cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
+    surf = cal._get_surface()
+    X = np.array([s["x0"] for s in g["calibrate_seed0_starts"]], dtype=float)
+    one, two = X[:1], X[1:3]
+    surf.fg_begin(one, 100.0, 0.05, N, model=fd_models(one), slot=2)
+    surf.fg_begin(two, 100.0, 0.05, N, model=fd_models(two), slot=3)
+    got2 = surf.fg_end(3)
+    got1 = surf.fg_end(2)
+    for got, Xi in ((got1, one), (got2, two)):
+        want = surf.fg(Xi, 100.0, 0.05, N, model=fd_models(Xi))
+        for u, v in zip(got, want):
+            assert np.array_equal(u, v)
+
+
 def test_characteristic_function_complex_phi(dh, cf_complex_golden):
     """DoubleHeston.characteristic_function at complex phi (double_heston.py:48-61 documents
     phi : complex) against the reference's values: 216 scalar points (damped shifts u - i alpha,
