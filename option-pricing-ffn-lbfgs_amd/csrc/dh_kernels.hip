@@ -2652,6 +2652,7 @@ struct dh_surface {
     int* tile_group = nullptr;
     double* group_T = nullptr;
     int2* groups = nullptr;
+    void* block = nullptr;  // the one device allocation every array above points into
 };
 
 namespace {
@@ -2872,13 +2873,13 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         HIP_TRY(hipGetLastError());
     }
     // small requests whose records were handed over from the host (dh_surface_fg_begin): the
-    // records in the kernel arguments, one-round in-block-prologue launches only
+    // records in the kernel arguments (in-block-prologue launches of the 4-wave build)
     if (ctx->kp_on < 0) {
         const char* e = std::getenv("DHCOS_KARG_PARAMS");
         ctx->kp_on = (e && e[0] == '0') ? 0 : 1;
     }
     if (ctx->kp_on && ctx->kp_src && A.P == ctx->kp_n && A.P <= kKargSets && r1 && !wide &&
-        !A.ahead && blocks < kPrologueKernelMinBlocks && !ctx->stamps_on && !A.exact) {
+        blocks < kPrologueKernelMinBlocks && !ctx->stamps_on && !A.exact) {
         KargParams pb{};
         std::memcpy(pb.v, ctx->kp_src, (size_t)A.P * DH_PARAM_STRIDE * sizeof(double));
         switch (t1) {
@@ -2887,6 +2888,11 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
             default: hipLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
         }
         HIP_TRY(hipGetLastError());
+        if (A.partials_only == 2) {
+            hipLaunchKernelGGL(loss_partials_kernel, dim3((unsigned)A.P), dim3(64), 0, st,
+                               (const double2*)A.part_sse, A.n_tiles, A.sse, A.n_bad);
+            HIP_TRY(hipGetLastError());
+        }
         return DH_OK;
     }
     // grids of many small blocks (C4: 28,672) gain from a fifth wave per SIMD to overlap the
@@ -3244,38 +3250,37 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
     s->max_group = max_group;
     s->strike_mode = strike_mode;
     s->has_mkt = mkt != nullptr;
-    const size_t m8 = std::max<size_t>(1, (size_t)M) * 8;
-    hipError_t e = hipSuccess;
-    auto alloc = [&](void** p, size_t bytes) {
-        if (e == hipSuccess) e = hipMalloc(p, std::max<size_t>(bytes, 16));
+    // every array in one device allocation, staged on the host and uploaded by one copy (one
+    // hipMalloc and one synchronous copy instead of nine of each: ~0.5 ms of a C3 calibration)
+    struct Part {
+        void** dst;
+        const void* src;
+        size_t bytes;
     };
-    alloc((void**)&s->K, m8);
-    alloc((void**)&s->T, m8);
-    alloc((void**)&s->mkt, m8);
-    alloc((void**)&s->call, std::max(1, M));
-    alloc((void**)&s->perm, std::max<size_t>(1, (size_t)M) * 4);
-    alloc((void**)&s->tiles, std::max<size_t>(1, tiles.size()) * sizeof(int2));
-    alloc((void**)&s->tile_group, std::max<size_t>(1, tile_group.size()) * sizeof(int));
-    alloc((void**)&s->group_T, std::max<size_t>(1, group_T.size()) * sizeof(double));
-    alloc((void**)&s->groups, std::max<size_t>(1, groups.size()) * sizeof(int2));
-    if (e == hipSuccess && M > 0) {
-        e = hipMemcpy(s->K, sK.data(), (size_t)M * 8, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(s->T, sT.data(), (size_t)M * 8, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(s->mkt, sm.data(), (size_t)M * 8, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(s->call, sc.data(), (size_t)M, hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(s->perm, perm.data(), (size_t)M * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(s->tiles, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(s->tile_group, tile_group.data(), tile_group.size() * sizeof(int),
-                          hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(s->group_T, group_T.data(), group_T.size() * sizeof(double),
-                          hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(s->groups, groups.data(), groups.size() * sizeof(int2),
-                          hipMemcpyHostToDevice);
+    const size_t m = (size_t)M;
+    const Part parts[] = {{(void**)&s->K, sK.data(), m * 8},
+                          {(void**)&s->T, sT.data(), m * 8},
+                          {(void**)&s->mkt, sm.data(), m * 8},
+                          {(void**)&s->call, sc.data(), m},
+                          {(void**)&s->perm, perm.data(), m * 4},
+                          {(void**)&s->tiles, tiles.data(), tiles.size() * sizeof(int2)},
+                          {(void**)&s->tile_group, tile_group.data(), tile_group.size() * sizeof(int)},
+                          {(void**)&s->group_T, group_T.data(), group_T.size() * sizeof(double)},
+                          {(void**)&s->groups, groups.data(), groups.size() * sizeof(int2)}};
+    size_t off[9], total = 0;
+    for (int i = 0; i < 9; ++i) {          // 256-byte aligned, >= 16 bytes each (empty surfaces)
+        off[i] = total;
+        total += (std::max<size_t>(parts[i].bytes, 16) + 255) & ~(size_t)255;
+    }
+    hipError_t e = hipMalloc(&s->block, total);
+    if (e == hipSuccess) {
+        for (int i = 0; i < 9; ++i) *parts[i].dst = (char*)s->block + off[i];
+        if (M > 0) {
+            std::vector<char> stage(total, 0);
+            for (int i = 0; i < 9; ++i)
+                if (parts[i].bytes) std::memcpy(stage.data() + off[i], parts[i].src, parts[i].bytes);
+            e = hipMemcpy(s->block, stage.data(), total, hipMemcpyHostToDevice);
+        }
     }
     if (e != hipSuccess) {
         dh_surface_destroy(s);
@@ -3288,9 +3293,7 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
 int dh_surface_destroy(dh_surface* s) {
     if (!s) return DH_OK;
     DeviceScope dev_scope(s->ctx ? s->ctx->device : 0);
-    for (void* p : {(void*)s->K, (void*)s->T, (void*)s->mkt, (void*)s->call, (void*)s->perm,
-                    (void*)s->tiles, (void*)s->tile_group, (void*)s->group_T, (void*)s->groups})
-        if (p) (void)hipFree(p);
+    if (s->block) (void)hipFree(s->block);
     delete s;
     return DH_OK;
 }

@@ -223,6 +223,7 @@ class DoubleHestonJumpCalibrator:
         self.device = device
         self._surface = None
         self._surface_ok = None    # False when an option_type is '' (every loss is then 1e10)
+        self._strikes = self._maturities = None   # _option_arrays
         self.loss_evals = 0        # param sets evaluated over the object's life (all starts)
 
     # ---- transforms (lbfgs_calibrator.py:62-116) ---------------------------------------
@@ -260,11 +261,19 @@ class DoubleHestonJumpCalibrator:
                 self._surface_ok = False
                 return None
             ctx = _native.default_context(self.device)
-            K = list(map(itemgetter("strike"), opts))
-            T = list(map(itemgetter("maturity"), opts))
+            K, T = self._option_arrays()
             self._surface = _native.Surface(ctx, K, T, flags, self.market_prices)
             self._surface_ok = True
         return self._surface if self._surface_ok else None
+
+    def _option_arrays(self):
+        """The options' strikes and maturities as NumPy arrays, built once (np.array of the
+        dicts' values: float64 for numbers, another dtype when a value is not one)."""
+        if self._strikes is None:
+            opts = self.market_options
+            self._strikes = np.array(list(map(itemgetter("strike"), opts)))
+            self._maturities = np.array(list(map(itemgetter("maturity"), opts)))
+        return self._strikes, self._maturities
 
     def _records(self, X: np.ndarray):
         P = x_to_model(X)
@@ -337,12 +346,25 @@ class DoubleHestonJumpCalibrator:
             for name in ("rho1", "rho2"):
                 params[name] = np.clip(params[name], -0.95, -0.3)
         else:
-            atm = [o for o in self.market_options if 0.95 < o["strike"] / self.spot < 1.05]
             iv = 0.04
-            if atm:
-                avg_p = np.mean([o["price"] for o in atm])
-                avg_t = np.mean([o["maturity"] for o in atm])
-                iv = max(0.01, min(0.1, (avg_p / self.spot) / np.sqrt(avg_t)))
+            K, T = self._option_arrays()
+            P = self.market_prices
+            if (K.dtype.kind in "fi" and T.dtype.kind in "fi" and P.dtype.kind in "fi"
+                    and isinstance(self.spot, (float, int))):
+                # the reference's ATM filter and means over arrays: the same IEEE division and
+                # comparisons per option, and np.mean of the same values in the same order
+                m = K / self.spot
+                atm = (0.95 < m) & (m < 1.05)
+                if atm.any():
+                    avg_p = np.mean(P[atm])
+                    avg_t = np.mean(T[atm])
+                    iv = max(0.01, min(0.1, (avg_p / self.spot) / np.sqrt(avg_t)))
+            else:                   # values that are not plain numbers: the reference's loop
+                atm = [o for o in self.market_options if 0.95 < o["strike"] / self.spot < 1.05]
+                if atm:
+                    avg_p = np.mean([o["price"] for o in atm])
+                    avg_t = np.mean([o["maturity"] for o in atm])
+                    iv = max(0.01, min(0.1, (avg_p / self.spot) / np.sqrt(avg_t)))
             params = {"v1_0": iv, "kappa1": 2.0, "theta1": iv, "sigma1": 0.4, "rho1": -0.6,
                       "v2_0": iv, "kappa2": 0.7, "theta2": iv, "sigma2": 0.25, "rho2": -0.4,
                       "lambda_j": 0.12, "mu_j": -0.03, "sigma_j": 0.07}
@@ -549,16 +571,14 @@ def _pipeline_surface(cal, n_starts, force=None):
 
 def _pipeline_groups(surf, n_starts):
     """How many groups (request slots, each on its own stream: _slot_ctx) the pipelined loop
-    splits the starts into: one per start (up to _native.FG_SLOTS) when one start's request is a
-    small grid (14 x tiles <= 256 blocks: C1), whose concurrent requests share the GPU; else two
-    (C2, C3: larger requests overlap less and each extra one costs device time).  Measured with the
-    native loop (round 5, calibrate(300, 3), medians of 7): C1 3.98 ms with three against 4.20 ms
-    with two, C2 4.75 / 4.64 ms, C3 8.91 / 8.68 ms.  $DHCOS_SCIPY_GROUPS overrides."""
+    splits the starts into: one per start, up to _native.FG_SLOTS.  A one-start request's 14
+    records then travel in its launch's kernel arguments (libdhcos KargParams) instead of mapped
+    host memory.  Measured with the native loop (round 5, calibrate(300, 3), medians of 7, one
+    box): C2 4.73 ms with three groups against 4.79 ms with two, C3 8.42 / 8.76 ms; before the
+    records moved to the arguments two groups were faster on C2 and C3 (4.64 / 4.75 ms,
+    8.68 / 8.91 ms) and three on C1 (3.98 / 4.20 ms).  $DHCOS_SCIPY_GROUPS overrides."""
     env = os.environ.get("DHCOS_SCIPY_GROUPS", "")
-    if env:
-        G = int(env)
-    else:
-        G = _native.FG_SLOTS if (N_PARAMS + 1) * max(1, surf.n_tiles) <= 256 else 2
+    G = int(env) if env else _native.FG_SLOTS
     return max(1, min(G, n_starts, _native.FG_SLOTS))
 
 

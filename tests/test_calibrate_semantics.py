@@ -117,3 +117,45 @@ def test_raising_start_costs_no_duplicate_evaluations(calib_golden):
     bad = [x for x in cal.seen if x[11] > -0.0315]
     assert len(ok) == len(ref.seen)                 # no point of a surviving start twice
     assert len(bad) == 1                            # the raising start: its first point only
+
+
+def _guess2_loop(cal):
+    """get_initial_guess(2)'s implied volatility as lbfgs_calibrator.py:211-222 forms it: the ATM
+    filter and the two means over lists of the option dicts' values."""
+    atm = [o for o in cal.market_options if 0.95 < o["strike"] / cal.spot < 1.05]
+    iv = 0.04
+    if atm:
+        avg_p = np.mean([o["price"] for o in atm])
+        avg_t = np.mean([o["maturity"] for o in atm])
+        iv = max(0.01, min(0.1, (avg_p / cal.spot) / np.sqrt(avg_t)))
+    return iv
+
+
+@pytest.mark.parametrize("case", ["floats", "int_strikes", "no_atm", "edges", "mixed_prices"])
+def test_atm_guess_over_arrays_equals_the_loop(case):
+    """The type-2 guess filters and averages over cached arrays: the same iv bits as the
+    reference's loop over the dicts, on float and int strikes, no ATM option, strikes on the
+    filter's edges (0.95 S and 1.05 S are out) and int/float prices."""
+    rs = np.random.RandomState({"floats": 1, "int_strikes": 2, "no_atm": 3, "edges": 4,
+                                "mixed_prices": 5}[case])
+    S = 100.0
+    n = 500
+    K = rs.uniform(70, 130, n)
+    if case == "int_strikes":
+        K = [int(k) for k in K]
+    elif case == "no_atm":
+        K = np.concatenate([rs.uniform(60, 94, n // 2), rs.uniform(106, 140, n - n // 2)])
+    elif case == "edges":
+        K = np.concatenate([[95.0, 105.0, 95.0000000001, 104.9999999999], K[4:]])
+    T = rs.uniform(0.05, 2.0, n)
+    P = rs.uniform(0.5, 30.0, n)
+    prices = [int(p) if (case == "mixed_prices" and i % 3 == 0) else float(p)
+              for i, p in enumerate(P)]
+    opts = [{"strike": k if isinstance(k, int) else float(k), "maturity": float(t), "price": p,
+             "option_type": "call"} for k, t, p in zip(K, T, prices)]
+    cal = DoubleHestonJumpCalibrator(S, 0.03, opts)
+    iv = _guess2_loop(cal)
+    x = cal.get_initial_guess(2)
+    assert x[0] == np.log(iv) and x[2] == np.log(iv)          # v1_0, theta1: log of iv
+    if case == "no_atm":
+        assert iv == 0.04
