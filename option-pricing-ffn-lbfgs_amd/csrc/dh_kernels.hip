@@ -33,6 +33,7 @@
 //   Validation ("exact") mode runs cos_exact_kernel instead: per-term CF + sincos in the
 //   reference's operation order, one wave per option.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <array>
 #include <rccl/rccl.h>   // types only: librccl is resolved at run time (dlopen)
 #include <dlfcn.h>
@@ -2629,6 +2630,12 @@ struct dh_ctx {
     const double* kp_src = nullptr;
     int64_t kp_n = 0;
     int kp_on = -1;
+    // and its completion event: recorded by the launch itself (hipExtLaunchKernel's stop event)
+    // when the fused kernel is the request's last launch; kp_done_set tells the caller
+    // ($DHCOS_EXT_EVENT=0: a separate hipEventRecord; ext_on: -1 not read yet)
+    hipEvent_t kp_done = nullptr;
+    bool kp_done_set = false;
+    int ext_on = -1;
     int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
                                // in loss_partials_kernel (-1: not read yet)
     std::vector<std::pair<std::array<int64_t, 3>, int>> resident_fused;
@@ -2882,12 +2889,18 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         blocks < kPrologueKernelMinBlocks && !ctx->stamps_on && !A.exact) {
         KargParams pb{};
         std::memcpy(pb.v, ctx->kp_src, (size_t)A.P * DH_PARAM_STRIDE * sizeof(double));
+        if (ctx->ext_on < 0) {
+            const char* e = std::getenv("DHCOS_EXT_EVENT");
+            ctx->ext_on = (e && e[0] == '0') ? 0 : 1;
+        }
+        hipEvent_t stop = (ctx->ext_on && A.partials_only != 2) ? ctx->kp_done : nullptr;
         switch (t1) {
-            case 64: hipLaunchKernelGGL((cos_fused_kernel<64, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
-            case 128: hipLaunchKernelGGL((cos_fused_kernel<128, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
-            default: hipLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
+            case 64: hipExtLaunchKernelGGL((cos_fused_kernel<64, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, nullptr, stop, 0, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
+            case 128: hipExtLaunchKernelGGL((cos_fused_kernel<128, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, nullptr, stop, 0, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
+            default: hipExtLaunchKernelGGL((cos_fused_kernel<256, 1, DH_FUSED_WAVES, true>), grid, block, lds, st, nullptr, stop, 0, A.prm, tsrc, A.groups, A.live_count, A.pre, tpp, A.paired, A, t2, pb); break;
         }
         HIP_TRY(hipGetLastError());
+        ctx->kp_done_set = stop != nullptr;
         if (A.partials_only == 2) {
             hipLaunchKernelGGL(loss_partials_kernel, dim3((unsigned)A.P), dim3(64), 0, st,
                                (const double2*)A.part_sse, A.n_tiles, A.sse, A.n_bad);
@@ -4591,13 +4604,17 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     // the records also travel in the fused launch's kernel arguments when they fit (KargParams)
     ctx->kp_src = (const double*)F.h_params.ptr;
     ctx->kp_n = (int64_t)P;
+    ctx->kp_done = F.done;
+    ctx->kp_done_set = false;
     rc = dh_surface_loss_dev(ctx, s, (const double*)F.h_params.dptr, (int)P, N, L,
                              (double*)F.h_loss.dptr, (int32_t*)((double*)F.h_loss.dptr + P),
                              nullptr, ctx->stream);
     ctx->kp_src = nullptr;
     ctx->kp_n = 0;
+    ctx->kp_done = nullptr;
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(F.done, ctx->stream));
+    if (!ctx->kp_done_set) HIP_TRY(hipEventRecord(F.done, ctx->stream));
+    ctx->kp_done_set = false;
     F.pending = true;
     return DH_OK;
 }
