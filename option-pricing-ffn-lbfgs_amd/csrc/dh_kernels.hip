@@ -3511,9 +3511,13 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
         std::memcpy(ctx->h_params.ptr, params, pb);
         double* h_sse = (double*)ctx->h_loss.ptr;
         int32_t* h_bad = (int32_t*)(h_sse + S);
+        ctx->kp_src = (const double*)ctx->h_params.ptr;     // <= 14 records: in the arguments
+        ctx->kp_n = S;
         rc = dh_surface_loss_dev(ctx, s, (const double*)ctx->h_params.dptr, S, N, L,
                                  (double*)ctx->h_loss.dptr, (int32_t*)((double*)ctx->h_loss.dptr + S),
                                  d_prices, ctx->stream);
+        ctx->kp_src = nullptr;
+        ctx->kp_n = 0;
         if (rc) return rc;
         if (prices && s->M > 0)
             HIP_TRY(hipMemcpyAsync(prices, d_prices, ob, hipMemcpyDeviceToHost, ctx->stream));

@@ -578,11 +578,12 @@ def test_fg_begin_end_slots(dh, calib_golden):
 
 @pytest.mark.parametrize("N", [64, 128, 256])
 def test_fg_begin_single_start_records_in_kernel_arguments(dh, calib_golden, N):
-    """A one-start asynchronous request (14 records) passes its records in the fused launch's
-    kernel arguments (KargParams) instead of mapped host memory; fg's synchronous request reads
-    them from memory.  Same bits, at each fused block width (N = 64 / 128 / 256), and a
-    two-start request (28 records, from memory) alongside in another slot."""
-    from dhcos.calibrator import fd_models
+    """A one-start request (14 records, asynchronous or synchronous) passes its records in the
+    fused launch's kernel arguments (KargParams) instead of mapped host memory.  Same bits as a
+    context that reads them from memory ($DHCOS_KARG_PARAMS=0), at each fused block width
+    (N = 64 / 128 / 256), and a two-start request (28 records, from memory) alongside."""
+    from dhcos import _native
+    from dhcos.calibrator import fd_models, resolve_call
     g = calib_golden
     cal = dh.DoubleHestonJumpCalibrator(100.0, 0.05, g["test_market"])
     surf = cal._get_surface()
@@ -592,10 +593,30 @@ def test_fg_begin_single_start_records_in_kernel_arguments(dh, calib_golden, N):
     surf.fg_begin(two, 100.0, 0.05, N, model=fd_models(two), slot=3)
     got2 = surf.fg_end(3)
     got1 = surf.fg_end(2)
-    for got, Xi in ((got1, one), (got2, two)):
-        want = surf.fg(Xi, 100.0, 0.05, N, model=fd_models(Xi))
-        for u, v in zip(got, want):
-            assert np.array_equal(u, v)
+    # the reference bits: a context that reads every record from memory ($DHCOS_KARG_PARAMS=0 is
+    # read by a context at its first launch)
+    old = os.environ.get("DHCOS_KARG_PARAMS")
+    os.environ["DHCOS_KARG_PARAMS"] = "0"
+    try:
+        ctx = _native.Context(surf.ctx.device)
+        mem = _native.Surface(ctx, [o["strike"] for o in g["test_market"]],
+                              [o["maturity"] for o in g["test_market"]],
+                              [resolve_call(o["option_type"]) for o in g["test_market"]],
+                              cal.market_prices)
+        for got, Xi in ((got1, one), (got2, two)):
+            want = mem.fg(Xi, 100.0, 0.05, N, model=fd_models(Xi))
+            for u, v in zip(got, want):
+                assert np.array_equal(u, v)
+            # and the synchronous request of <= 14 records (records in the arguments too)
+            for u, v in zip(surf.fg(Xi, 100.0, 0.05, N, model=fd_models(Xi)), want):
+                assert np.array_equal(u, v)
+        mem.close()
+        ctx.close()
+    finally:
+        if old is None:
+            os.environ.pop("DHCOS_KARG_PARAMS", None)
+        else:
+            os.environ["DHCOS_KARG_PARAMS"] = old
 
 
 def test_characteristic_function_complex_phi(dh, cf_complex_golden):
