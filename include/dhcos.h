@@ -293,6 +293,38 @@ int dh_gen_assemble(const double* model, const double* noise, const double* spot
                     const double* k_rel, int64_t n_samples, int n_opt, double* market,
                     double* loss, double* strikes);
 
+/* The generator's whole batch path on the device (replaces synthetic_generator.py:98-157's
+ * per-sample loop).  The host keeps only the serial part of NumPy's legacy stream
+ * -- the MT19937 twister and the walk over the polar acceptances, which give each sample its
+ * first double -- on a team of threads; per 65,536-sample chunk the device re-creates the
+ * stream's words, draws each sample's uniforms and normals (glibc's log restated), runs the AR(1)
+ * blend (alpha; 1 - alpha as the reference forms it) and the spot walk from spot0 (returns
+ * normal(ret_mu, ret_sigma)), prices the grid's options (`grid`: strikes in percent of each
+ * sample's spot, DH_STRIKE_PCT_SPOT; rate r, COS N, L) and forms market = model + normal(0,
+ * noise_sigma) * model, the per-sample loss (np.mean's bits) and strikes = k_rel[j] spot / 100.
+ * Every value is the reference loop's bit for bit; the RNG state arguments (np.random.get_state()
+ * fields) are advanced in place to where that loop leaves them.  Host outputs (page-locked ones,
+ * dh_host_alloc, move by DMA): params [n][13], spots [n], market, model, strikes [n][M], loss [n],
+ * and dates [n][10] UCS-4 ('YYYY-MM-DD' weekdays from day first_day, dh_gen_dates) unless null.
+ * stats [8] (optional): seconds from the call's start at which the twister and the walk ended,
+ * the first chunk was issued and the call returned; AR(1) segments re-run serially; key blocks
+ * bounded / used; chunks.  1 <= M <= 128.                                                        */
+int dh_gen_device(dh_ctx* ctx, const dh_surface* grid, uint32_t* mt_key, int32_t* mt_pos,
+                  int32_t* has_gauss, double* cached_gauss, int64_t n_samples, const double* lo,
+                  const double* hi, double alpha, double spot0, double ret_mu, double ret_sigma,
+                  double noise_sigma, double r, int N, double L, const double* k_rel,
+                  int64_t first_day, double* params, double* spots, double* market,
+                  double* model, double* loss, double* strikes, uint32_t* dates, double* stats);
+/* The device's restatement of glibc's log (the legacy gauss's, dh_gen_device) over x[n]: its
+ * GPU test against libm.                                                                         */
+int dh_gen_log(dh_ctx* ctx, const double* x, int64_t n, double* out);
+/* Page-locked host memory from a process-wide cache (hipHostMalloc; a freed block serves the next
+ * request of up to 1.25x its size): the generator's output arrays.  dh_host_cache_trim releases
+ * the cached blocks.                                                                             */
+int dh_host_alloc(size_t bytes, void** out);
+int dh_host_free(void* p);
+int dh_host_cache_trim(void);
+
 /* ---- paired pricing: option i under param set i ------------------------------------------- */
 /* out[i] = price of (K[i], T[i], is_call[i]) under params[i]; replaces a loop of single
  * DoubleHeston(...).pricing(N) calls (double_heston.py:160-192).                              */

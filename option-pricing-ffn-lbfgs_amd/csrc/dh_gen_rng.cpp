@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "dhcos.h"
+#include "dh_gen_rng.h"
 
 namespace {
 
@@ -368,9 +369,17 @@ struct ParDraw {
     int64_t n = 0, n_opt = 0, n_chunks = 0, max_t = 0, max_blocks = 0;
     // chunk c covers samples [starts[c], starts[c + 1]) (starts[n_chunks] = n)
     std::vector<int64_t> starts;
-    // published by the twister: keys of generations 64 b
+    // published by the twister: keys of generations 64 b (in `snaps`, or in a caller's buffer:
+    // snap points at the one in use), and mirrored to keys_ready_ext if set
     std::vector<uint32_t> snaps;
+    uint32_t* snap = nullptr;
     std::atomic<int64_t> snaps_ready{0};
+    std::atomic<int64_t>* keys_ready_ext = nullptr;
+    // per-sample walk records for the device draw (dhgen::Located), if set: sample i's first
+    // double and the source of its cached gauss value, published in located_ext
+    int64_t* t_out = nullptr;
+    int64_t* cs_out = nullptr;
+    std::atomic<int64_t>* located_ext = nullptr;
     // acceptance bits of the candidate pair at double t, by parity: bit (t >> 1) of bits[t & 1]
     std::vector<std::atomic<uint64_t>> bits[2];
     std::vector<std::atomic<uint8_t>> block_done;
@@ -402,7 +411,7 @@ struct ParDraw {
 
     // key of generation g into k (from the block's snapshot, twisted forward)
     void gen_key(int64_t g, uint32_t* k) const {
-        std::memcpy(k, snaps.data() + (g / kGensPerBlock) * kMtN, sizeof(uint32_t) * kMtN);
+        std::memcpy(k, snap + (g / kGensPerBlock) * kMtN, sizeof(uint32_t) * kMtN);
         LegacyRng r;
         std::memcpy(r.key, k, sizeof(r.key));
         for (int64_t i = 0; i < g % kGensPerBlock; ++i) mt_twist(r.key);
@@ -418,7 +427,7 @@ struct ParDraw {
             return;
         }
         const int64_t g0 = ready > 0 ? (ready - 1) * kGensPerBlock : 0;
-        std::memcpy(k, ready > 0 ? snaps.data() + (ready - 1) * kMtN : key0,
+        std::memcpy(k, ready > 0 ? snap + (ready - 1) * kMtN : key0,
                     sizeof(uint32_t) * kMtN);
         for (int64_t i = g0; i < g; ++i) mt_twist(k);
     }
@@ -455,8 +464,9 @@ void par_twister(ParDraw& P) {
         if (P.walk_done.load(std::memory_order_acquire) || P.failed.load()) return;
         if (b > 0)
             for (int i = 0; i < kGensPerBlock; ++i) mt_twist(r.key);
-        std::memcpy(P.snaps.data() + b * kMtN, r.key, sizeof(r.key));
+        std::memcpy(P.snap + b * kMtN, r.key, sizeof(r.key));
         P.snaps_ready.store(b + 1, std::memory_order_release);
+        if (P.keys_ready_ext) P.keys_ready_ext->store(b + 1, std::memory_order_release);
     }
 }
 
@@ -516,7 +526,7 @@ void par_bits(ParDraw& P, int64_t b, BitsScratch& S) {
     // raw key words of generations 64 b .. 64 b + 64 (the next block's first words close the
     // block's last pairs), tempered in place by the body
     LegacyRng r;
-    std::memcpy(r.key, P.snaps.data() + b * kMtN, sizeof(r.key));
+    std::memcpy(r.key, P.snap + b * kMtN, sizeof(r.key));
     const int64_t nw = kBlockWords + kMtN;
     S.w.resize(nw);
     for (int gi = 0; gi <= kGensPerBlock; ++gi) {
@@ -575,6 +585,11 @@ void par_walk(ParDraw& P, int hg0) {
     bool ok = true;
     int64_t c = 0;
     for (int64_t i = 0; i < P.n && ok; ++i) {
+        if (P.t_out) {                                    // the device draw's per-sample records
+            P.t_out[i] = t;
+            P.cs_out[i] = hg ? last_pair : -2;            // (last_pair -1: the entry's value)
+            if ((i & 1023) == 1023) P.located_ext->store(i + 1, std::memory_order_release);
+        }
         while (c < P.n_chunks && P.starts[c] == i) {     // (equal starts: empty chunks)
             P.chunk_t[c] = t;
             P.chunk_hg[c] = hg;
@@ -604,6 +619,10 @@ void par_walk(ParDraw& P, int hg0) {
     P.t_end = t;
     P.lp_end = last_pair;
     P.hg_end = hg;
+    if (P.t_out && ok && t < P.max_t) {
+        P.t_out[P.n] = t;
+        P.located_ext->store(P.n + 1, std::memory_order_release);
+    }
     P.walk_done.store(true, std::memory_order_release);
 }
 
@@ -687,10 +706,18 @@ void par_chunk(ParDraw& P, int64_t c, const double* lo, const double* range,
     P.chunk_done[c].store(1, std::memory_order_release);
 }
 
+// stream bound: twice the expected doubles (acceptance pi/4) plus slack; a walk past it (never
+// seen: ~thousands of standard deviations) falls back to the sequential draw
+void stream_bounds(int pos0, int64_t n_samples, int n_opt, int64_t& max_t, int64_t& max_blocks) {
+    const double per_sample = 13.0 + 2.0 * ((n_opt + 2) / 2) / 0.7853981633974483;
+    max_t = (int64_t)(2.0 * per_sample * (double)n_samples) + (1 << 20);
+    max_blocks = (pos0 + 2 * max_t) / kBlockWords + 2;
+}
+
 // The stream geometry and buffers of a parallel pass over n_samples from g's state, with chunk
 // starts `starts` (sorted; starts[0] = 0, the last entry n_samples)
 void par_setup(ParDraw& P, const LegacyRng& g, int64_t n_samples, int n_opt,
-               std::vector<int64_t> starts) {
+               std::vector<int64_t> starts, uint32_t* keys = nullptr) {
     LegacyRng e = g;
     if (e.pos == kMtN) e.twist();
     P.pos0 = e.pos;
@@ -699,12 +726,13 @@ void par_setup(ParDraw& P, const LegacyRng& g, int64_t n_samples, int n_opt,
     P.n_opt = n_opt;
     P.starts = std::move(starts);
     P.n_chunks = (int64_t)P.starts.size() - 1;
-    // stream bound: twice the expected doubles (acceptance pi/4) plus slack; a walk past it
-    // (never seen: ~thousands of standard deviations) falls back to the sequential draw
-    const double per_sample = 13.0 + 2.0 * ((n_opt + 2) / 2) / 0.7853981633974483;
-    P.max_t = (int64_t)(2.0 * per_sample * (double)n_samples) + (1 << 20);
-    P.max_blocks = (P.pos0 + 2 * P.max_t) / kBlockWords + 2;
-    P.snaps.resize((size_t)P.max_blocks * kMtN);
+    stream_bounds(P.pos0, n_samples, n_opt, P.max_t, P.max_blocks);
+    if (keys) {
+        P.snap = keys;
+    } else {
+        P.snaps.resize((size_t)P.max_blocks * kMtN);
+        P.snap = P.snaps.data();
+    }
     const int64_t nwords = (P.max_t / 2) / 64 + 2;
     for (int p = 0; p < 2; ++p) {
         std::vector<std::atomic<uint64_t>> v(nwords);
@@ -1174,6 +1202,85 @@ int gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss, double* cach
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// The host part of the device draw (dh_gen_rng.h): the twister, the bit workers and the walk of
+// the parallel draw, with the walk's per-sample records (first double, cached-value source) and
+// the keys in the caller's buffers, published as they are written.
+// ---------------------------------------------------------------------------------------------
+namespace dhgen {
+
+void locate_geometry(Located& L) {
+    L.pos0 = L.pos == kMtN ? 0 : L.pos;
+    stream_bounds(L.pos0, L.n, L.n_opt, L.max_t, L.max_blocks);
+}
+
+void locate_run(Located& L) {
+    const double t_start = now_s();
+    LegacyRng g;
+    std::memcpy(g.key, L.key, sizeof(g.key));
+    g.pos = L.pos;
+    g.has_gauss = L.has_gauss ? 1 : 0;
+    g.gauss = L.gauss;
+    const LegacyRng entry = g;
+    ParDraw P;
+    par_setup(P, g, L.n, L.n_opt, std::vector<int64_t>{L.n}, L.keys);
+    P.t_out = L.t;
+    P.cs_out = L.cs;
+    P.located_ext = &L.located;
+    P.keys_ready_ext = &L.keys_ready;
+    {
+        Team team(std::max(3, team_size()));
+        team.run([&](int w) {
+            if (w == 1) {
+                par_twister(P);
+                L.s_twister = now_s() - t_start;
+                w = 2;
+            }
+            if (w == 0) {
+                par_walk(P, g.has_gauss ? 1 : 0);
+                L.s_walk = now_s() - t_start;
+                return;
+            }
+            par_worker(P, false, nullptr, nullptr, 0.0, 0.0, 0.0, nullptr, nullptr, nullptr);
+        });
+    }
+    if (P.failed.load()) {
+        L.state.store(-1, std::memory_order_release);
+        return;
+    }
+    par_final_state(P, entry, g);
+    std::memcpy(L.key_end, g.key, sizeof(g.key));
+    L.pos_end = g.pos;
+    L.has_gauss_end = g.has_gauss;
+    L.gauss_end = g.gauss;
+    L.state.store(1, std::memory_order_release);
+}
+
+void locate_extend_keys(Located& L, int64_t blocks) {
+    blocks = std::min(blocks, L.max_blocks);
+    int64_t b = L.keys_ready.load(std::memory_order_acquire);
+    if (b >= blocks) return;
+    uint32_t k[kMtN];
+    if (b == 0) {
+        LegacyRng e;
+        std::memcpy(e.key, L.key, sizeof(e.key));
+        e.pos = L.pos;
+        if (e.pos == kMtN) e.twist();
+        std::memcpy(k, e.key, sizeof(k));
+        std::memcpy(L.keys, k, sizeof(k));
+        b = 1;
+    } else {
+        std::memcpy(k, L.keys + (b - 1) * kMtN, sizeof(k));
+    }
+    for (; b < blocks; ++b) {
+        for (int i = 0; i < kGensPerBlock; ++i) mt_twist(k);
+        std::memcpy(L.keys + b * kMtN, k, sizeof(k));
+    }
+    L.keys_ready.store(blocks, std::memory_order_release);
+}
+
+}  // namespace dhgen
 
 extern "C" int dh_gen_draw(uint32_t* mt_key, int32_t* mt_pos, int32_t* has_gauss,
                            double* cached_gauss, int64_t n_samples, const double* lo,

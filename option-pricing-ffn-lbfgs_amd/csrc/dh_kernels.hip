@@ -2581,6 +2581,9 @@ int option_tpt(int max_nopt, int N, int cap) {
 
 }  // namespace
 
+struct GenBufs;                         // dh_gen_device.h
+void gen_bufs_release(dh_ctx* ctx);
+
 struct dh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -2639,6 +2642,7 @@ struct dh_ctx {
     int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
                                // in loss_partials_kernel (-1: not read yet)
     std::vector<std::pair<std::array<int64_t, 3>, int>> resident_fused;
+    GenBufs* gen = nullptr;    // the generator's device draw (dh_gen_device)
 };
 
 struct dh_surface {
@@ -3147,6 +3151,7 @@ int dh_ctx_destroy(dh_ctx* ctx) {
     ctx->h_pairs.release();
     for (hipEvent_t e : ctx->lb_ev)
         if (e) (void)hipEventDestroy(e);
+    gen_bufs_release(ctx);
     for (auto& F : ctx->fg) {
         F.h_params.release();
         F.h_loss.release();
@@ -4849,3 +4854,5 @@ extern "C" int dh_allgather_best(dh_comm* c, const double* rec, int rows, int wi
     if (rc) return rc;
     return dh_best_start(all, (int64_t)rows * c->world, width, col_start, col_fun, best);
 }
+
+#include "dh_gen_device.h"

@@ -99,6 +99,14 @@ SIGNATURES = {
     "dh_gen_drawn_samples": (C.c_int, [C.POINTER(C.c_int64)]),
     "dh_gen_assemble": (C.c_int, [_dp, _dp, _dp, _dp, C.c_int64, C.c_int, _dp, _dp, _dp]),
     "dh_gen_dates": (C.c_int, [C.c_int64, C.c_int64, _vp]),
+    "dh_gen_device": (C.c_int, [_vp, _vp, C.POINTER(C.c_uint32), _i32p, _i32p, _dp, C.c_int64,
+                                _dp, _dp, C.c_double, C.c_double, C.c_double, C.c_double,
+                                C.c_double, C.c_double, C.c_int, C.c_double, _dp, C.c_int64,
+                                _vp, _vp, _vp, _vp, _vp, _vp, _vp, _dp]),
+    "dh_gen_log": (C.c_int, [_vp, _vp, C.c_int64, _vp]),
+    "dh_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(_vp)]),
+    "dh_host_free": (C.c_int, [_vp]),
+    "dh_host_cache_trim": (C.c_int, []),
     "dh_price_batch": (C.c_int, [_vp, _dp, C.c_int64, _dp, _dp, _i8p, C.c_int, C.c_int,
                                  C.c_double, _dp]),
     "dh_loss_batch": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp, _i8p, _dp, C.c_int, C.c_double,
@@ -879,6 +887,10 @@ def gen_dates(first_day, n):
 
 
 _tls = threading.local()
+# the device resolved under each initialised process group (resolve_device): fixed at the group's
+# first resolution, so that the library's own CUDA tensors (collectives on the LOCAL_RANK GPU)
+# cannot move a later resolution to torch's default device 0
+_group_device = {}
 
 
 def resolve_device(device: int | None = None) -> int:
@@ -898,19 +910,32 @@ def resolve_device(device: int | None = None) -> int:
     torch = sys.modules.get("torch")
     dist = getattr(torch, "distributed", None) if torch is not None else None
     if dist is not None and dist.is_available() and dist.is_initialized():
+        try:
+            group = dist.distributed_c10d._get_default_group()
+        except Exception:              # noqa: BLE001 -- an older torch without the accessor
+            group = None
+        key = id(group)
+        hit = _group_device.get(key)
+        if hit is not None and hit[0] is group:
+            return hit[1]
+        dev = None
         if torch.cuda.is_available():
-            try:
-                bound = dist.distributed_c10d._get_default_group().bound_device_id
-            except Exception:          # noqa: BLE001 -- an older torch without the attribute
-                bound = None
+            bound = getattr(group, "bound_device_id", None)
             if bound is not None and bound.type == "cuda" and bound.index is not None:
-                return int(bound.index)
-            if torch.cuda.is_initialized():
-                return int(torch.cuda.current_device())
-        local = os.environ.get("LOCAL_RANK")
-        if local not in (None, ""):
-            n = device_count()
-            return int(local) % n if n > 0 else int(local)
+                dev = int(bound.index)
+            elif torch.cuda.is_initialized():
+                # the rank set up its CUDA state before its first call here: its current device
+                dev = int(torch.cuda.current_device())
+        if dev is None:
+            local = os.environ.get("LOCAL_RANK")
+            if local not in (None, ""):
+                n = device_count()
+                dev = int(local) % n if n > 0 else int(local)
+            else:
+                dev = 0
+        if group is not None:
+            _group_device[key] = (group, dev)
+        return dev
     return 0
 
 
@@ -939,6 +964,84 @@ class pinned:
         return False
 
 
+class _PinnedBlock:
+    """A dh_host_alloc block exposed through the array interface; the block returns to the
+    library's page-locked cache when the last array over it is freed."""
+
+    def __init__(self, shape, dtype):
+        self.nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+        ptr = _vp()
+        _check(load().dh_host_alloc(self.nbytes, C.byref(ptr)))
+        self.ptr = ptr.value
+        self.__array_interface__ = {"shape": tuple(int(d) for d in shape), "typestr": dtype.str,
+                                    "data": (self.ptr, False), "version": 3}
+
+    def __del__(self):
+        lib = _lib
+        if lib is not None and getattr(self, "ptr", None):
+            lib.dh_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_empty(shape, dtype=np.float64) -> np.ndarray:
+    """An uninitialised C-contiguous array in page-locked host memory from the library's cache
+    (dh_host_alloc): device copies into it run as DMA, and a freed array's block serves the next
+    request of its size without a new allocation or page faults."""
+    dtype = np.dtype(dtype)
+    if isinstance(shape, (int, np.integer)):
+        shape = (int(shape),)
+    if int(np.prod(shape, dtype=np.int64)) == 0:
+        return np.empty(shape, dtype=dtype)
+    return np.asarray(_PinnedBlock(shape, dtype))
+
+
+def host_cache_trim():
+    """Release the page-locked blocks the cache holds (dh_host_cache_trim)."""
+    _check(load().dh_host_cache_trim())
+
+
+def gen_log(x, ctx=None) -> np.ndarray:
+    """dh_gen_log: the device restatement of glibc's log (the legacy gauss's) over x."""
+    x = _f64(x).ravel()
+    out = np.empty_like(x)
+    ctx = ctx or default_context()
+    _check(load().dh_gen_log(ctx.handle, x.ctypes.data if x.size else None, x.size,
+                             out.ctypes.data if x.size else None))
+    return out
+
+
+def gen_device(surf, n_samples, lo, hi, alpha, spot0, ret_mu, ret_sigma, noise_sigma, r, k_rel,
+               N=128, L=10.0, first_day=None, stats=None):
+    """dh_gen_device on NumPy's global legacy RandomState: the generator's samples drawn, blended,
+    priced on ``surf`` (its grid, strikes in percent of each sample's spot) and assembled on the
+    device; np.random's state advanced exactly as the reference's per-sample calls would.  The
+    outputs are page-locked arrays (pinned_empty).  -> dict(params, spots, market, model, loss,
+    strikes, dates ('<U10', or None when first_day is None))."""
+    name, key, pos, has_gauss, cached = np.random.get_state()
+    if name != "MT19937":
+        raise NativeError(f"unsupported bit generator {name}")
+    key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+    c_pos, c_has, c_cached = C.c_int32(int(pos)), C.c_int32(int(has_gauss)), C.c_double(cached)
+    n, m = int(n_samples), int(surf.M)
+    k_rel = _f64(k_rel).reshape(-1)
+    if k_rel.size != m:
+        raise NativeError("gen_device: one strike percentage per option of the grid")
+    out = {"params": pinned_empty((n, 13)), "spots": pinned_empty(n),
+           "market": pinned_empty((n, m)), "model": pinned_empty((n, m)),
+           "loss": pinned_empty(n), "strikes": pinned_empty((n, m)),
+           "dates": pinned_empty(n, "U10") if first_day is not None else None}
+    st = np.zeros(8) if stats is None else stats
+    addr = {k: (v.ctypes.data if v is not None and v.size else None) for k, v in out.items()}
+    _check(load().dh_gen_device(
+        surf.ctx.handle, surf.handle, key.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(c_pos),
+        C.byref(c_has), C.byref(c_cached), n, _ptr(_f64(lo)), _ptr(_f64(hi)), float(alpha),
+        float(spot0), float(ret_mu), float(ret_sigma), float(noise_sigma), float(r), int(N),
+        float(L), _ptr(k_rel), int(first_day or 0), addr["params"], addr["spots"],
+        addr["market"], addr["model"], addr["loss"], addr["strikes"], addr["dates"], _ptr(st)))
+    np.random.set_state((name, key, c_pos.value, c_has.value, c_cached.value))
+    return out
+
+
 def default_context(device: int | None = None) -> Context:
     """Per-thread cached context on ``device`` (default: resolve_device())."""
     device = resolve_device(device)
@@ -958,4 +1061,5 @@ __all__ = ["gen_draw", "gen_assemble", "gen_dates", "gen_locate", "gen_draw_loca
            "STRIKE_PCT_SPOT", "PATH_AUTO", "PATH_SPLIT", "PATH_FUSED", "PATH_GEN",
            "LIB_PATH",
            "SIGNATURES",
-           "Comm", "comm_id", "best_start", "COMM_ID_BYTES", "FgChannel", "pinned"]
+           "Comm", "comm_id", "best_start", "COMM_ID_BYTES", "FgChannel", "pinned",
+           "pinned_empty", "host_cache_trim", "gen_device", "gen_log"]

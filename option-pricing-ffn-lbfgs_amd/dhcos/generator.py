@@ -3,17 +3,22 @@
 Reference: src/data/synthetic_generator.py:25-234.  Per sample the reference draws 13 uniforms,
 blends them AR(1) (alpha = 0.9) into the previous sample, random-walks the spot, prices a 5 x 3
 call grid one option at a time and adds 2% Gaussian noise to each price.  Pricing consumes no
-randomness, so this implementation
+randomness, and the samples' positions in the stream depend on the data only through the polar
+method's acceptances, so this implementation
 
-  1. draws every random number on the host in the reference's order from the legacy global
-     ``np.random`` stream (13 uniforms, then one spot normal for i > 0, then 15 noise normals)
-     and runs the AR(1) and spot recursions -- natively (``dh_gen_draw``: NumPy's MT19937 and
-     legacy uniform / polar-gauss restated, state taken from and handed back to ``np.random``,
-     ~10x the per-sample NumPy loop, which stays as ``draw_paths_numpy`` for the tests),
-  2. (the recursions run inside the same native loop),
-  3. prices all samples x options in one launch per chunk on the GPU (strikes formed on the device
-     as K_relative * spot / 100.0, exactly the reference's expression, :125),
-  4. applies the noise and the per-sample loss with the reference's NumPy expressions.
+  1. the host runs only the serial part of the legacy ``np.random`` stream: NumPy's MT19937
+     recurrence and the walk over the polar acceptances, which gives each sample its first
+     double (state taken from and handed back to ``np.random``);
+  2. the device re-creates the stream's words, draws every sample's uniforms and normals in the
+     reference's order (13 uniforms, one spot normal for i > 0, 15 noise normals; glibc's log
+     restated so the gauss values are NumPy's bits), runs the AR(1) blend and the spot walk,
+  3. prices all samples x options (strikes K_relative * spot / 100.0, exactly the reference's
+     expression, :125) and applies the noise and the per-sample loss with the reference's NumPy
+     expressions, chunk by chunk behind the host walk, into page-locked output arrays
+     (``_native.gen_device``).
+
+``draw="host"`` keeps the round-4 pipeline (``dh_gen_draw``: the same draws on the host's
+threads, priced chunk by chunk); ``draw_paths_numpy`` is the per-sample NumPy loop of the tests.
 
 Output: ``list[CalibrationResult]`` pickled to ``save_path`` (as the reference), or, with
 ``as_arrays=True``, a dict of columnar arrays (no per-sample Python objects, for 10^6 samples).
@@ -163,6 +168,51 @@ def draw_paths_numpy(n_samples, strikes=STRIKES_PCT, maturities=MATURITIES):
     return params, spots, noise
 
 
+def grid_surface(ctx, strikes=STRIKES_PCT, maturities=MATURITIES):
+    """The call grid (T outer, K inner -- the reference's loop order) as a surface of strikes in
+    percent of each sample's spot, cached on the context (one per grid: creating and destroying
+    it per call cost a device allocation and a synchronising free per call).
+    -> (surface, K_rel [m], T [m])."""
+    Krel = np.tile(np.asarray(strikes, dtype=np.float64), len(maturities))
+    T = np.repeat(np.asarray(maturities, dtype=np.float64), len(strikes))
+    grids = ctx.__dict__.setdefault("_grid_surfaces", {})
+    key = (Krel.tobytes(), T.tobytes())
+    surf = grids.get(key)
+    if surf is None:
+        surf = grids[key] = _native.Surface(ctx, Krel, T, np.ones(T.size, dtype=np.int8),
+                                            strike_mode=_native.STRIKE_PCT_SPOT)
+    return surf, Krel, T
+
+
+# the last device draw's timings (seconds from the call's start; dh_gen_device's stats): when the
+# twister and the walk (the host's serial part) ended, when the first chunk went to the device,
+# when the call returned
+last_device_stats = {}
+
+
+def generate_device(n_samples, N=128, device=None, strikes=STRIKES_PCT, maturities=MATURITIES,
+                    r=RISK_FREE):
+    """The whole batch path on the device (dh_gen_device) from np.random's state, which it
+    advances as the reference's loop does.  -> dict(params, spots, market, model, loss, strikes,
+    dates ('<U10'), maturities)."""
+    ctx = _native.default_context(device)
+    surf, Krel, T = grid_surface(ctx, strikes, maturities)
+    lo, hi = _ranges()
+    n = int(n_samples)
+    # the device forms the dates while years have four digits (n <= ~2M samples from 2022)
+    dates_dev = n <= 2_000_000
+    st = np.zeros(8)
+    out = _native.gen_device(surf, n, lo, hi, ALPHA, SPOT_BASE, 0.0003, 0.01, 0.02, r, Krel, N=N,
+                             first_day=18995 if dates_dev else None, stats=st)
+    if not dates_dev:
+        out["dates"] = trading_dates_array(n)
+    last_device_stats.clear()
+    last_device_stats.update(twister_s=st[0], walk_s=st[1], first_chunk_s=st[2], total_s=st[3],
+                             ar1_segments_rerun=int(st[4]), chunks=int(st[7]))
+    out["maturities"] = T
+    return out
+
+
 def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES, r=RISK_FREE,
                chunk=1 << 18, device=None, ready=None, on_chunk=None):
     """GPU: price every sample's call grid (T outer, K inner -- the reference's loop order).
@@ -170,16 +220,7 @@ def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES,
     _native.GenDraw); the chunks, and so the launches and the bits, are the same either way.
     ``on_chunk(s, e, out)``, if given, is called after rows [s, e) of ``out`` are priced."""
     ctx = _native.default_context(device)
-    Krel = np.tile(np.asarray(strikes, dtype=np.float64), len(maturities))
-    T = np.repeat(np.asarray(maturities, dtype=np.float64), len(strikes))
-    # the grid's surface lives with the context (one per grid): creating and destroying it per
-    # call cost a device allocation and a synchronising free per call
-    grids = ctx.__dict__.setdefault("_grid_surfaces", {})
-    key = (Krel.tobytes(), T.tobytes())
-    surf = grids.get(key)
-    if surf is None:
-        surf = grids[key] = _native.Surface(ctx, Krel, T, np.ones(T.size, dtype=np.int8),
-                                            strike_mode=_native.STRIKE_PCT_SPOT)
+    surf, Krel, T = grid_surface(ctx, strikes, maturities)
     n = params.shape[0]
     out = np.empty((n, T.size))
     if ready is not None:
@@ -207,10 +248,18 @@ def price_grid(params, spots, N=128, strikes=STRIKES_PCT, maturities=MATURITIES,
 def generate_synthetic_calibrations(n_samples: int = 500,
                                     save_path: str = "lbfgs_calibrations_synthetic.pkl", *,
                                     N: int = 128, device=None, as_arrays: bool = False,
-                                    verbose: bool = True):
-    """Generate ``n_samples`` synthetic calibrations (synthetic_generator.py:25-234).  The native
-    draw runs on a worker thread and the GPU prices each chunk of samples as soon as the draw has
-    finished it (the draw dominates a 1M-sample run, profiles/r03_generator_e2e.json)."""
+                                    verbose: bool = True, draw: str = "device"):
+    """Generate ``n_samples`` synthetic calibrations (synthetic_generator.py:25-234).  By default
+    the draws, recursions, pricing and assembly run on the device behind the host's serial walk of
+    the RNG stream (generate_device); ``draw="host"``: the native host draw on a worker thread,
+    each chunk priced on the GPU as soon as the draw has finished it."""
+    if draw not in ("device", "host"):
+        raise ValueError("draw must be 'device' or 'host'")
+    if draw == "device" and int(n_samples) > 0:
+        o = generate_device(n_samples, N=N, device=device)
+        return assemble(o["params"], o["spots"], None, o["model"], save_path, as_arrays=as_arrays,
+                        verbose=verbose, N=N, assembled=(o["market"], o["loss"], o["strikes"]),
+                        dates=o["dates"])
     d = draw_paths_async(n_samples)
     dates = []                         # the columnar dates depend on n only: formed meanwhile
     t_dates = threading.Thread(target=lambda: dates.append(trading_dates_array(n_samples)))

@@ -254,11 +254,13 @@ def test_missing_outcome_record_never_wins():
 
 
 def test_resolve_device_under_process_group(monkeypatch):
-    """Under torch.distributed on a multi-GPU node: a gloo job that never touched CUDA puts
-    rank LOCAL_RANK on its own GPU (not every rank on torch's default GPU 0); once the rank has
-    a CUDA state, torch's current device wins over LOCAL_RANK -- set_device(5), and also an
-    explicit set_device(0) with LOCAL_RANK = 3 (the caller's own rank-to-GPU map).  (GPUs
-    simulated: 8 visible.)"""
+    """Under torch.distributed on a multi-GPU node the device is resolved once per process group
+    (ADVICE r5): a gloo job that never touched CUDA puts rank LOCAL_RANK on its own GPU (not every
+    rank on torch's default GPU 0), and the library's own CUDA tensors that follow (the first
+    collective's tensors on that GPU initialise CUDA without a set_device, leaving torch's current
+    device at 0) do not move later calls to GPU 0; a rank that set its device before its first
+    call (set_device(5), or an explicit set_device(0) under LOCAL_RANK = 3) keeps that device.
+    (GPUs simulated: 8 visible.)"""
     import torch
     from dhcos import _native
     monkeypatch.delenv("DHCOS_DEVICE", raising=False)
@@ -268,16 +270,34 @@ def test_resolve_device_under_process_group(monkeypatch):
     cur = {"dev": 0, "init": False}
     monkeypatch.setattr(torch.cuda, "current_device", lambda: cur["dev"])
     monkeypatch.setattr(torch.cuda, "is_initialized", lambda: cur["init"])
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
-    dist.init_process_group("gloo", rank=0, world_size=1)
-    try:
+
+    def group(then):
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        try:
+            then()
+        finally:
+            dist.destroy_process_group()
+
+    def no_cuda_state_first():
         assert _native.resolve_device() == 3          # no CUDA state: LOCAL_RANK
+        cur.update(dev=0, init=True)                  # the first collective's tensors init CUDA
+        assert _native.resolve_device() == 3          # ... and do not move the rank to GPU 0
         cur.update(dev=5, init=True)
-        assert _native.resolve_device() == 5          # set_device(5)
-        cur.update(dev=0, init=True)
-        assert _native.resolve_device() == 0          # set_device(0) under LOCAL_RANK = 3
-        monkeypatch.setenv("LOCAL_RANK", "11")
-        cur.update(dev=0, init=False)
-        assert _native.resolve_device() == 3          # modulo the visible GPUs
-    finally:
-        dist.destroy_process_group()
+        assert _native.resolve_device() == 3          # fixed for the group's lifetime
+
+    def set_device_first(dev):
+        def run():
+            cur.update(dev=dev, init=True)            # the rank's own set_device before any call
+            assert _native.resolve_device() == dev
+            cur.update(dev=7)
+            assert _native.resolve_device() == dev
+        return run
+
+    cur.update(dev=0, init=False)
+    group(no_cuda_state_first)
+    group(set_device_first(5))
+    group(set_device_first(0))                        # set_device(0) under LOCAL_RANK = 3
+    monkeypatch.setenv("LOCAL_RANK", "11")
+    cur.update(dev=0, init=False)
+    group(lambda: _native.resolve_device() == 3 or pytest.fail("modulo the visible GPUs"))
