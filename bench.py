@@ -472,31 +472,55 @@ def bench_generator(args, cfg, world, rank, dev, coll, stream, cpu=None):
         dist.destroy_process_group()
 
 
-def generator_end_to_end(world, rank, coll, n_samples=1_000_000):
+def generator_end_to_end(world, rank, coll, n_samples=1_000_000, host_path=False):
     """generate_synthetic_calibrations(n_samples, as_arrays=True) end to end under
-    np.random.seed(0): the reference's RNG draws (native legacy-NumPy stream), its 5 x 3 call
-    grid priced on the GPUs (sharded at N > 1), noise and per-sample losses."""
+    np.random.seed(0): the reference's RNG draws (legacy-NumPy stream: its serial part -- the
+    MT19937 twister and the walk over the polar acceptances -- on the host, everything else on the
+    device at N = 1), its 5 x 3 call grid priced on the GPUs (sharded at N > 1), noise and
+    per-sample losses.  host_draw_seconds = when the host's serial part ended within the call;
+    host_path: also one call of the round-4 host-draw pipeline, for comparison."""
     from dhcos import generator as G
-    from dhcos.distributed import generate_sharded
+    from dhcos.distributed import generate_sharded, last_generate_stats
     if world > 1:
         dist.barrier()
     np.random.seed(0)
     t0 = time.perf_counter()
     out = generate_sharded(n_samples, None, as_arrays=True, verbose=False)
     dt = time.perf_counter() - t0
-    t_draw = None
-    if rank == 0:                       # the host-draw share of it
+    stages = None
+    if world == 1:
+        st = dict(G.last_device_stats)
+        stages = {k: st[k] for k in ("twister_s", "walk_s", "first_chunk_s", "total_s")}
+        stages["ar1_segments_rerun"] = st["ar1_segments_rerun"]
+        host_s = st["walk_s"]
+    else:
+        # per-stage seconds of every rank (generate_sharded's instrumentation): the max over ranks
+        sec = last_generate_stats.get("seconds", {})
+        keys = sorted(sec)
+        v = torch.tensor([sec[k] for k in keys], dtype=torch.float64, device=coll)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        stages = {k: float(x) for k, x in zip(keys, v.tolist())}
+        host_s = stages.get("locate_broadcast")
+    dt = _max_over_ranks(dt, world, coll)
+    del out
+    t_host = None
+    if host_path and world == 1:
         np.random.seed(0)
         t1 = time.perf_counter()
-        G.draw_paths(n_samples)
-        t_draw = time.perf_counter() - t1
-    dt = _max_over_ranks(dt, world, coll)
+        G.generate_synthetic_calibrations(n_samples, None, as_arrays=True, verbose=False,
+                                          draw="host")
+        t_host = time.perf_counter() - t1
     if rank != 0:
         return None
-    return {"samples": n_samples, "options_per_sample": int(out["model_prices"].shape[1]),
-            "seconds": dt, "samples_per_sec": n_samples / dt, "host_draw_seconds": t_draw,
-            "call": "generate_synthetic_calibrations(1_000_000, as_arrays=True), np.random.seed(0)"
-                    + (", sharded over ranks" if world > 1 else "")}
+    r = {"samples": n_samples, "options_per_sample": len(G.STRIKES_PCT) * len(G.MATURITIES),
+         "seconds": dt, "samples_per_sec": n_samples / dt, "host_draw_seconds": host_s,
+         "stages_s": stages,
+         "call": "generate_synthetic_calibrations(1_000_000, as_arrays=True), np.random.seed(0)"
+                 + (", sharded over ranks (generate_sharded)" if world > 1 else
+                    ", device draw (dh_gen_device)")}
+    if t_host is not None:
+        r["host_draw_pipeline_seconds"] = t_host
+    return r
 
 
 def request_bench(cfg, steps, warmup, world, rank, dev, coll, stream, starts_rank=None):
@@ -641,13 +665,66 @@ def c1_calibration_leg(world, coll):
     return out
 
 
+REFERENCE_C1 = {"final_loss": 1.0196869185631994e-07, "iterations": 33,
+                "message": "CONVERGENCE: RELATIVE REDUCTION OF F <= FACTR*EPSMCH",
+                "seconds_measured_here": [132.1, 139.5], "readme_seconds": 117.8,
+                "source": "SURVEY.md 3.2 / 6 (the reference run in the build container), README.md:16"}
+REFERENCE_C1_START0 = {"final_loss": 9.761042426892e-05, "iterations": 0, "message": "ABNORMAL: ",
+                       "seconds_measured_here": 27.7, "source": "SURVEY.md 3.2 (start 0)"}
+
+
+def reference_market():
+    """The reference's own calibration market (tests/test_suite.py:274-302): 15 clean calls, K in
+    {90 .. 110}, T in {0.25, 0.5, 1}, priced by the reference at its true parameters, S0 = 100,
+    r = 0.05 (tests/golden/calib.json, written by make_golden.py from the reference)."""
+    with open(os.path.join(ROOT, "tests", "golden", "calib.json")) as fh:
+        return json.load(fh)["test_market"], 100.0, 0.05
+
+
+def c1_reference_market_leg(world, coll):
+    """configs[0] on the reference's own market: calibrate(300, 1) and calibrate(300, 3) under
+    np.random.seed(0), N = 128, both drivers, beside the reference's outcome and time."""
+    opts, S0, r = reference_market()
+    out = {"workload": "configs[0] on the reference's market (tests/test_suite.py:274-302): 15 "
+                       "clean calls, N=128, np.random.seed(0)",
+           "reference_3_starts": REFERENCE_C1, "reference_start_0": REFERENCE_C1_START0}
+    for ns in (1, 3):
+        for drv in ("scipy", "device"):
+            c = calib_leg(S0, r, opts, 128, ns, world, coll, drv, reps=5)
+            ref = REFERENCE_C1 if ns == 3 else REFERENCE_C1_START0
+            rs = ref["seconds_measured_here"]
+            c["speedup_vs_reference_measured"] = (np.mean(rs) if isinstance(rs, list) else rs) / \
+                c["seconds"]
+            out[f"calibrate_{ns}_start{'s' if ns > 1 else ''}_{drv}"] = c
+    return out
+
+
+def c4_sharded_leg(world, coll, reps=3):
+    """configs[3]: 64 independent multi-start L-BFGS-B starts on the 1,024-option N = 256
+    surface, calibrate_sharded: the starts dealt over the ranks, one all-gather (RCCL under
+    nccl) of every start's record and the strict-< best start, inside the timed region; strong
+    scaling (64 starts in all at any world size)."""
+    cfg = CONFIGS["c4"]
+    opts, S0, r = make_surface(cfg["nK"], cfg["nT"], N=cfg["N"], put_itm=cfg["put_itm"])
+    out = {"workload": cfg["workload"], "scaling": "strong", "starts": cfg["starts"],
+           "world_size_seen": world}
+    for drv in ("scipy", "device"):
+        out[drv] = calib_leg(S0, r, opts, cfg["N"], cfg["starts"], world, coll, drv, reps=reps)
+    return out
+
+
 def c5_leg(dev, stream, rank):
     """The metric's own N = 128: the generator batch (1M param sets x 32 options)."""
     cfg = CONFIGS["c5"]
     g = gen_batch(cfg["P"], cfg["N"], 5, 2, dev, stream, rank)
     rf = gen_roofline(g, "c5")
-    e2e = [generator_end_to_end(1, rank, None) for _ in range(3)]
+    generator_end_to_end(1, rank, None)          # first call: the output cache's allocations
+    e2e = [generator_end_to_end(1, rank, None, host_path=(i == 1)) for i in range(3)]
+    host = [r.get("host_draw_pipeline_seconds") for r in e2e if "host_draw_pipeline_seconds" in r]
     e2e = sorted(e2e, key=lambda r: r["seconds"])[1]            # the median of 3 API calls
+    e2e.pop("host_draw_pipeline_seconds", None)
+    if host:
+        e2e["host_draw_pipeline_seconds"] = host[0]
     return {"workload": cfg["workload"], "prices_per_sec": g["value"],
             "ms_per_batch": g["ms_per_step"], "kernel_ms": g["ker_ms"], "steps": 5,
             "roofline_frac": rf["frac"], "hbm": rf["hbm"], "generator_end_to_end": e2e}
@@ -773,7 +850,14 @@ def main():
                                                       args.no_calib)
         side["c5_generator_n128"] = c5_leg(dev, stream, rank)
         if not args.no_calib:
+            side["c1_reference_market"] = c1_reference_market_leg(world, coll)
             side["c1_calibration"] = c1_calibration_leg(world, coll)
+    # the north star's two 8-GPU configurations, at every world size (N = 1 is their baseline):
+    # C4's 64 starts sharded with the RCCL gather, C5's generator sharded end to end
+    if args.config == "c3" and not args.no_side and not args.no_calib:
+        side["c4_sharded_64_starts"] = c4_sharded_leg(world, coll)
+        if world > 1:
+            side["c5_generator_sharded"] = generator_end_to_end(world, rank, coll)
 
     # ---- calibrations/sec: one full calibration of the same surface; at N > 1 its starts are
     # sharded over the ranks (dhcos.distributed; the config's starts per GPU, weak scaling; c4:

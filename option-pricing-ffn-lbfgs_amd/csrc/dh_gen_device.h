@@ -232,47 +232,71 @@ __device__ double ar1_run(const double* __restrict__ praw, int j, int64_t a, int
 }
 
 // The spot walk (:112-116) spot_i = spot_{i-1} (1 + ret_i) over [i0, i1), serial: lane 0 of one
-// wave runs the chain, one v_mul_f64 per sample with the multiplier in scalar registers (wave-
-// uniform loads through the scalar cache, 16 at a time), and leaves each value in LDS; the wave
-// then stores the batch of 64 with one coalesced store.  The multiplier of sample 0 is 1.0
-// (gen_draw_kernel), which keeps spot0; mret holds 64 readable doubles past i1 (their products
-// land past the batch and are not stored).
+// wave runs the chain, one dependent v_mul_f64 per sample, on the batch's 64 multipliers staged in
+// LDS, and leaves each value in LDS; the wave then stores the batch with one coalesced store.  The
+// multipliers are loaded by the whole wave kSpotAhead batches ahead (a register ring), so the
+// chain never waits on memory.  The multiplier of sample 0 is 1.0 (gen_draw_kernel), which keeps
+// spot0; loads past i1 are clamped (their products are not stored).
+constexpr int kSpotAhead = 8;
+
 __global__ __launch_bounds__(64) void gen_spot_kernel(const double* __restrict__ mret, int64_t i0,
                                                       int64_t i1, double spot0, double r,
                                                       double* __restrict__ carry_spot,
                                                       double* __restrict__ spots,
                                                       double* __restrict__ rec) {
 #pragma clang fp contract(off)
+    __shared__ double mv[64];
     __shared__ double sv[64];
+    // the chain shares its SIMD with the pricing kernel's waves of the chunk before: top issue
+    // priority, so that its one dependent multiply per sample issues as soon as it is ready
+    __builtin_amdgcn_s_setprio(3);
     const int lane = threadIdx.x;
+    const int64_t last = i1 - 1;
     double s = i0 == 0 ? spot0 : carry_spot[0];
-    for (int64_t b = i0; b < i1; b += 64) {
-        const int nb = i1 - b < 64 ? (int)(i1 - b) : 64;
-        if (lane == 0) {
-            double v = s;
+    double ring[kSpotAhead];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                double m[16];
+    for (int k = 0; k < kSpotAhead; ++k) {
+        const int64_t i = i0 + 64 * k + lane;
+        ring[k] = mret[i < last ? i : last];
+    }
+    for (int64_t base = i0; base < i1; base += 64 * kSpotAhead) {
 #pragma unroll
-                for (int q = 0; q < 16; ++q) m[q] = mret[b + 16 * g + q];
+        for (int k = 0; k < kSpotAhead; ++k) {
+            const int64_t b = base + 64 * k;
+            const double m = ring[k];
+            const int64_t ia = b + 64 * kSpotAhead + lane;
+            ring[k] = mret[ia < last ? ia : last];
+            if (b < i1) {
+                const int nb = i1 - b < 64 ? (int)(i1 - b) : 64;
+                mv[lane] = m;
+                wave_sync();
+                if (lane == 0) {
+                    double ml[64];                    // all 64 reads issued ahead of the chain
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    v = v * m[q];
-                    sv[16 * g + q] = v;
+                    for (int l = 0; l < 64; ++l) ml[l] = mv[l];
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    double v = s, out[64];        // the chain alone, then the 64 stores
+#pragma unroll
+                    for (int l = 0; l < 64; ++l) {
+                        v = v * ml[l];
+                        out[l] = v;
+                    }
+#pragma unroll
+                    for (int l = 0; l < 64; ++l) sv[l] = out[l];
                 }
+                wave_sync();
+                const double out = sv[lane];
+                s = sv[nb - 1];
+                if (lane < nb) {
+                    const int64_t i = b + lane;
+                    spots[i] = out;
+                    rec[i * DH_PARAM_STRIDE + 13] = out;
+                    rec[i * DH_PARAM_STRIDE + 14] = r;
+                    rec[i * DH_PARAM_STRIDE + 15] = 0.0;
+                }
+                wave_sync();
             }
         }
-        wave_sync();
-        const double out = sv[lane];
-        s = sv[nb - 1];
-        if (lane < nb) {
-            const int64_t i = b + lane;
-            spots[i] = out;
-            rec[i * DH_PARAM_STRIDE + 13] = out;
-            rec[i * DH_PARAM_STRIDE + 14] = r;
-            rec[i * DH_PARAM_STRIDE + 15] = 0.0;
-        }
-        wave_sync();
     }
     if (lane == 0) carry_spot[0] = s;
 }
@@ -599,7 +623,13 @@ int dh_gen_device(dh_ctx* ctx, const dh_surface* grid, uint32_t* mt_key, int32_t
     GenBufs& G = *ctx->gen;
     if (!G.s_price) HIP_TRY(hipStreamCreateWithFlags(&G.s_price, hipStreamNonBlocking));
     if (!G.s_copy) HIP_TRY(hipStreamCreateWithFlags(&G.s_copy, hipStreamNonBlocking));
-    if (!G.s_spot) HIP_TRY(hipStreamCreateWithFlags(&G.s_spot, hipStreamNonBlocking));
+    if (!G.s_spot) {
+        // the spot walk is the pipeline's serial chain: a high-priority stream, which also puts it
+        // on a hardware queue of its own (not behind the copies of the stream sharing a queue)
+        int lo_prio = 0, hi_prio = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+        HIP_TRY(hipStreamCreateWithPriority(&G.s_spot, hipStreamNonBlocking, hi_prio));
+    }
 
     // the host part: twister, bit workers, walk (on their own threads from here on)
     std::unique_ptr<dhgen::Located> Lp(new dhgen::Located());

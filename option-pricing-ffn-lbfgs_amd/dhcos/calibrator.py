@@ -616,8 +616,13 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
     order = [list(range(n))] if lockstep else [[s] for s in range(n)]
     surf = _pipeline_surface(cal, n, pipeline) if (lockstep and pipeline is not False) else None
     with _single_threaded_blas():
-        loop = _scipy_loop()
+        # cal.request_trace (a list; tests): every request's (start, x, f, g) in the order the
+        # starts consumed them -- recorded by the Python loops, which the native loop equals bit
+        # for bit (tests/test_gpu_parity.py::test_native_loop_equals_python_loop).  The native
+        # loop is loaded only where a native surface will use it.
+        traced = getattr(cal, "request_trace", None) is not None
         if surf is not None:
+            loop = None if traced else _scipy_loop()
             G = _pipeline_groups(surf, n)
             groups = [list(range(k, n, G)) for k in range(G)]
             cal.pipeline_groups = groups
@@ -626,11 +631,19 @@ def run_starts(cal: DoubleHestonJumpCalibrator, x0s, maxiter: int, lockstep: boo
             else:
                 _advance_pipelined(cal, surf, gens, states, outcomes, groups)
         else:
-            nsurf = _native_surface(cal, max(len(g) for g in order)) if loop else None
-            if nsurf is not None:
+            nsurf = None if traced else _native_surface(cal, max(len(g) for g in order))
+            loop = _scipy_loop() if nsurf is not None else None
+            if loop is not None:
                 launches = 0
                 for group in order:
-                    _run_native(loop, cal, nsurf, x0s, [group], maxiter, states, outcomes)
+                    # one native run per group over the group's own starts (ids remapped), so
+                    # the sequential starts cost O(n) setup, not O(n^2)
+                    sub = [None] * len(group)
+                    _run_native(loop, cal, nsurf, [x0s[s] for s in group],
+                                [list(range(len(group)))], maxiter, [states[s] for s in group],
+                                sub)
+                    for j, s in enumerate(group):
+                        outcomes[s] = sub[j]
                     launches += cal.lockstep_launches
                 cal.lockstep_launches = launches
             else:
@@ -734,7 +747,8 @@ def _advance(cal, gens, states, order, outcomes):
                     if not ids:
                         continue
                 launches += 1
-                _consume(states, gens, pending, outcomes, ids, f0, G, lows)
+                _consume(states, gens, pending, outcomes, ids, f0, G, lows,
+                         getattr(cal, "request_trace", None))
     finally:
         if busy:                       # unwinding with the slot's request in flight
             try:
@@ -744,9 +758,13 @@ def _advance(cal, gens, states, order, outcomes):
     cal.lockstep_launches = launches
 
 
-def _consume(states, gens, pending, outcomes, ids, f0, G, lows):
-    """A request's results to its starts' generators (the bookkeeping of _advance)."""
+def _consume(states, gens, pending, outcomes, ids, f0, G, lows, trace=None):
+    """A request's results to its starts' generators (the bookkeeping of _advance); trace (a
+    list) gets each start's (start, x, f, g)."""
     for j, sid in enumerate(ids):
+        if trace is not None:
+            trace.append((sid, np.array(pending[sid], dtype=np.float64), float(f0[j]),
+                          np.array(G[j], dtype=np.float64)))
         st = states[sid]
         st.n_calls += N_PARAMS + 1
         if lows[j] < st.best_loss:
@@ -819,7 +837,8 @@ def _advance_pipelined(cal, surf, gens, states, outcomes, groups):
                 f0, G, lows = chans[k].end()
                 busy[k] = False
                 launches += 1
-                _consume(states, gens, pending, outcomes, ids, f0, G, lows)
+                _consume(states, gens, pending, outcomes, ids, f0, G, lows,
+                         getattr(cal, "request_trace", None))
                 submit(k)
     finally:
         for k in range(n_groups):

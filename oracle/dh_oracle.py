@@ -52,15 +52,39 @@ def _heston_factor(u, tau, kappa, theta, sigma, rho):
     return B, A
 
 
-def cf(u, tau, prm, r, q=0.0):
+def _heston_factor_stable(u, tau, kappa, theta, sigma, rho):
+    """_heston_factor's (B_j, A_j) without its cancellation at small sigma -- NOT the reference's
+    operation order: a probe of how far the reference's own arithmetic is from the exact value
+    (tests/test_gpu_shadow.py).  beta - d = -sigma^2 u (u + i) / (beta + d), B = -u (u + i)(1 - e)
+    / D, log((1 - g e)/(1 - g)) = log(1 + w), w = (beta - d)(1 - e) / (2 d), D = (beta + d) -
+    (beta - d) e: the same quantities, no division of an O(sigma^2) difference by sigma^2."""
+    beta = kappa - rho * sigma * 1j * u
+    uu = u * (u + 1j)
+    d = np.sqrt(beta ** 2 + sigma ** 2 * uu)
+    bp = beta + d
+    c = uu / bp                                   # -(beta - d) / sigma^2
+    bm = -c * sigma ** 2
+    e = np.exp(-d * tau)
+    D = bp - bm * e
+    B = -uu * (1 - e) / D
+    w = bm * (1 - e) / (2 * d)
+    logq = 0.5 * np.log1p(2 * w.real + (w.real ** 2 + w.imag ** 2)) + \
+        1j * np.arctan2(w.imag, 1 + w.real)
+    A = kappa * theta * (-c * tau - 2 * logq / sigma ** 2)
+    return B, A
+
+
+def cf(u, tau, prm, r, q=0.0, stable=False):
     """phi(u) = exp(A + B1 v01 + B2 v02) * phi_jump(u)   (double_heston.py:82-96).
 
     ``u`` may be a scalar or an ndarray; the drift term carries the jump compensator
-    lambda (exp(mu + sigma_j^2/2) - 1) and no log(S0) term.
+    lambda (exp(mu + sigma_j^2/2) - 1) and no log(S0) term.  stable: the factors in the
+    cancellation-free form (_heston_factor_stable; a probe, not the reference's arithmetic).
     """
     v01, k1, t1, s1, r1, v02, k2, t2, s2, r2, lam, muj, sj = prm
-    B1, A1 = _heston_factor(u, tau, k1, t1, s1, r1)
-    B2, A2 = _heston_factor(u, tau, k2, t2, s2, r2)
+    hf = _heston_factor_stable if stable else _heston_factor
+    B1, A1 = hf(u, tau, k1, t1, s1, r1)
+    B2, A2 = hf(u, tau, k2, t2, s2, r2)
     comp = np.exp(muj + 0.5 * sj ** 2) - 1
     A = (r - q - lam * comp) * 1j * u * tau
     A = A + A1
@@ -210,6 +234,66 @@ def price_surface(prm, S0, K, T, r, is_call, N=128, q=0.0):
     terms = np.real(phi * np.exp(-1j * u * A)) * V
     terms[:, 0] *= 0.5
     return np.exp(-r * T) * np.sum(terms, axis=1)
+
+
+def price_surface_grouped(prm, S0, K, T, r, is_call, N=128, q=0.0, stable=False):
+    """price_surface with the characteristic function evaluated once per distinct (T, a, b) --
+    the reference evaluates it per option (double_heston.py:168), on the same u_k = k pi / (b - a)
+    and tau = T for every option of such a group, so the values are the same; everything per
+    option (the range, chi / psi, V, the sum) is price_surface's expressions.  The trajectory-
+    shadowing tests' checker at 10,000 options x N = 512 (tests/test_gpu_shadow.py;
+    tests/test_oracle_golden.py holds it to price_surface).  stable: the CF in the
+    cancellation-free form (cf(stable=True)), the exact-value probe of the shadowing tests."""
+    K = np.asarray(K, dtype=np.float64).reshape(-1)
+    T = np.asarray(T, dtype=np.float64).reshape(-1)
+    call = np.broadcast_to(np.asarray(is_call, dtype=bool), K.shape)
+    xK = np.log(K / S0)
+    v01, k1, t1, s1, r1, v02, k2, t2, s2, r2, lam, muj, sj = prm
+    c1a, c2a = _factor_cumulants(T, r, v01, k1, t1, s1, r1)       # trunc_range, per option
+    c1b, c2b = _factor_cumulants(T, r, v02, k2, t2, s2, r2)
+    c1 = c1a + c1b + lam * T * muj
+    c2 = c2a + c2b + lam * T * (sj ** 2 + muj ** 2)
+    half = 10.0 * np.sqrt(np.abs(c2))
+    a = np.minimum(c1 - half, xK - 0.1)
+    b = np.maximum(c1 + half, xK + 0.1)
+    k = np.arange(N, dtype=np.float64)[None, :]
+    key = np.stack([T, a, b], axis=1)
+    uniq, inv = np.unique(key, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    ug = k * np.pi / (uniq[:, 2] - uniq[:, 1])[:, None]
+    phi_g = cf(ug, uniq[:, 0][:, None], prm, r, q, stable=stable)
+    A_g = uniq[:, 1][:, None]
+    rot_g = phi_g * np.exp(-1j * ug * A_g)                        # phi(u_k) e^{-i u_k a} per group
+    u = ug[inv]
+    c = np.where(call, xK, a)[:, None]
+    d = np.where(call, b, xK)[:, None]
+    A = a[:, None]
+    ed, ec = np.exp(d), np.exp(c)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        cd, cc = np.cos(u * (d - A)), np.cos(u * (c - A))
+        sd, sc = np.sin(u * (d - A)), np.sin(u * (c - A))
+        ch = (1.0 / (1 + u ** 2)) * (cd * ed - cc * ec + u * sd * ed - u * sc * ec)
+        ps = (1.0 / u) * (sd - sc)
+    ch[:, 0] = (ed - ec)[:, 0]
+    ps[:, 0] = (d - c)[:, 0]
+    scale = (2.0 / (b - a))[:, None]
+    Kc = K[:, None]
+    V = np.where(call[:, None], scale * (S0 * ch - Kc * ps), scale * (Kc * ps - S0 * ch))
+    terms = np.real(rot_g[inv]) * V
+    terms[:, 0] *= 0.5
+    return np.exp(-r * T) * np.sum(terms, axis=1)
+
+
+def loss_surface(x, K, T, is_call, mkt, spot, r, N=128):
+    """compute_loss (lbfgs_calibrator.py:118-177) on a surface through price_surface_grouped:
+    (loss, prices); 1e10 on any NaN / inf / <= 0 price (Q5)."""
+    p = to_params(x)
+    with np.errstate(all="ignore"):
+        model = price_surface_grouped(p, spot, K, T, r, is_call, N)
+        if not np.all(np.isfinite(model)) or np.any(model <= 0):
+            return INVALID_LOSS, model
+        rel = (model - mkt) / mkt
+        return np.mean(rel ** 2) + feller(p), model
 
 
 def price_many(params, S0, K, T, r, is_call, N=128, q=0.0, scalar=False):

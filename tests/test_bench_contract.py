@@ -106,3 +106,30 @@ def test_bench_rccl_ranks_need_their_gpus():
     out = _bench_rc(["--gpus", "2", "--config", "c1", "--no-cpu", "--no-calib"])
     assert out.returncode != 0
     assert "needs 2 visible GPUs" in out.stderr
+
+
+@pytest.mark.gpu
+def test_bench_side_legs_two_ranks():
+    """The north star's 8-GPU configurations in the N > 1 line, rehearsed with
+    two gloo ranks on the box's one GPU: C4 (64 starts sharded with the gather of their records,
+    both drivers, strong scaling) and C5 (generate_sharded end to end, with the ranks' stage
+    times), each reporting the world it saw."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29541",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c3", "--steps", "3",
+           "--warmup", "1", "--no-cpu", "--backend", "gloo"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["world_size_seen"] == 2
+    c4 = line["c4_sharded_64_starts"]
+    assert c4["world_size_seen"] == 2 and c4["starts"] == 64 and c4["scaling"] == "strong"
+    for drv in ("scipy", "device"):
+        assert c4[drv]["starts"] == 64 and c4[drv]["calibrations_per_sec"] > 0
+        assert c4[drv]["final_loss"] < 1e9
+    c5 = line["c5_generator_sharded"]
+    assert c5["samples"] == 1_000_000 and c5["seconds"] > 0 and "sharded" in c5["call"]
+    assert set(c5["stages_s"]) >= {"locate_broadcast", "draw", "price", "gather"}
