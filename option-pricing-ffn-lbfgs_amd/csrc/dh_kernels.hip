@@ -95,7 +95,9 @@ struct PriceArgs {
                             // (invalid flag in the sign bit) and ends (no hand-off); the step
                             // kernel forms the sums.  2: multi-round fused requests: every task
                             // stores its (partial, invalid count) pair and ends; loss_partials_kernel
-                            // then forms the sums as the hand-off's last task would
+                            // then forms the sums as the hand-off's last task would.  3: the same
+                            // pairs as epoch-tagged granules (gran), summed by the grid's last
+                            // P blocks in the same launch (tail_sums)
     int M;                  // options in the (sorted) option arrays
     int N;
     double L;
@@ -120,13 +122,18 @@ struct PriceArgs {
     double tail;            // tail_delta's scale: kTailScale, or -1 (dh_ctx_set_tail_cut(0): every
                             // term summed); set by launch_price
     // prologues ahead (fused kernel, requests of more than one round of resident blocks): block
-    // q < ahead_stride forms the prologue constants of tables q + j ahead_stride (j = 1 ..
-    // kAheadMax) into ahead[.][kTabC] and then sets ahead_flag[.] = ahead_epoch; a later block
-    // whose flag holds this launch's epoch loads its constants instead of forming them
+    // q < ahead_stride (dispatch index) forms the truncation ranges and K_cf of the blocks
+    // q + j ahead_stride (j = 1 .. kAheadMax) into ahead[.][kAheadRec] and then sets ahead_flag[.]
+    // = ahead_epoch << 32 | K_cf; a later block whose flag holds this launch's epoch re-forms its
+    // constants from the record instead of running the cumulant chain and the CF-cut test
     double* ahead;
-    unsigned* ahead_flag;
+    unsigned long long* ahead_flag;   // epoch << 32 | K_cf of the table's record
     int ahead_stride;       // 0: off
     unsigned ahead_epoch;
+    // partials_only == 3: [P * n_tiles][2] granules (epoch-tagged halves of each task's pair)
+    unsigned long long* gran;
+    int remap;              // fused kernel: dispatch index -> table by XCD (xcd_table), else 0
+    int unused_pad;
 };
 
 // w_k of table q sits at table_w(A, q)[k * table_step(A)].  The small-tile option kernel has one
@@ -552,7 +559,7 @@ struct FusedKargsKP {       // cos_fused_kernel<..., true>'s argument list
     int tpt2;
     KargParams pb;
 };
-constexpr int kFusedParamsKernargOff = 368;
+constexpr int kFusedParamsKernargOff = 384;
 static_assert(offsetof(FusedKargsKP, pb) == kFusedParamsKernargOff, "param block kernarg offset");
 static_assert(sizeof(FusedKargsKP) + 256 <= 4096, "kernel arguments over 4 KiB");
 
@@ -560,6 +567,23 @@ static_assert(sizeof(FusedKargsKP) + 256 <= 4096, "kernel arguments over 4 KiB")
 // like any other, with no branch on the pointer (a branch made the compiler wait for it at the
 // kernel's entry)
 __device__ const int kLiveOne = 1;
+
+// The table (p * tpp + g) the fused grid's block of dispatch index b prices.  With A.remap the
+// blocks that share an XCD (b and b + 8: MI355X_MICROARCH.md, round-robin dispatch, observed, for
+// speed only) take, in dispatch order, one contiguous run of the tables in maturity-major order
+// (g * P + p): each XCD's L2 then holds ~1/8 of the option arrays, and the blocks running together
+// on an XCD stage the same maturity group's options.  A bijection onto the grid's tables for any
+// grid size, so any placement gives the same bits.
+__device__ __forceinline__ int64_t xcd_table(const PriceArgs& A, int tpp, int64_t b) {
+    if (!A.remap) return b;
+    const unsigned nb = gridDim.x;
+    const unsigned x = (unsigned)b & 7u, pos = (unsigned)b >> 3;
+    const unsigned per = nb >> 3, extra = nb & 7u;
+    const unsigned t = x * per + min(x, extra) + pos;        // maturity-major rank
+    const unsigned np = nb / (unsigned)tpp;
+    const unsigned g = t / np, p = t - g * np;
+    return (int64_t)p * tpp + g;
+}
 
 // The truncation range of table q (trunc_unclamped's bits) with the two variance factors'
 // cumulants on alternate lanes: table_prologue_wave's first step, and the whole of what
@@ -691,11 +715,14 @@ __device__ __forceinline__ int cf_cut_group8(const dh::Params& P, double T, doub
 // ----------------------------------------------------------------------------------------------
 constexpr int kAheadMax = 8;       // later tables per first-round block: 8-lane groups of a wave
 // What travels per later table: the prologue's values that cost a transcendental or a cumulant
-// chain -- a, b, e^b, e^a, the clamp bounds' slots 25 and 26, e^{-rT}, the CF drift and K_cf --
-// at ahead[q * kAheadRec + i] (one 128-byte line per table, the writer group's 8 lanes storing 8
-// of them in one coalesced store); the reader re-forms the other slots (2/(b - a), pi/(b - a), the
-// factors' constants, S0, r, T, the group) from the parameters by the same expressions.
-constexpr int kAheadRec = 16;
+// chain -- a, b, e^b, e^a, the clamp bounds' slots 25 and 26, e^{-rT} and the CF drift -- at
+// ahead[q * kAheadRec + i] (one 64-byte record per table, the writer group's 8 lanes storing it in
+// one coalesced store), and K_cf in the low half of the table's 64-bit flag (its high half the
+// launch's epoch); the reader re-forms the cheap slots (2/(b - a), pi/(b - a), the factors'
+// constants, S0, r, T, the group) from the parameters by the same expressions.  (Round 5 sent K_cf
+// in the record, one 128-byte line per table: 541 KB written per C3 request.  Sending (a, b) alone
+// and re-forming the six exponentials in the reader halved the writes again but cost C3 1.3 us.)
+constexpr int kAheadRec = 8;
 // v of lane (lane & ~7) | l: the 8-lane group's broadcast
 __device__ __forceinline__ double grp8_bcast(double v, int l) {
     const int src = ((int)__lane_id() & ~7) | l;
@@ -714,7 +741,8 @@ __device__ __forceinline__ double agent_load(const double* p) {
 }
 
 // The later table of 8-lane group lane / 8 of first-round block q0: q0 + (j + 1) R (act: it
-// exists; an inactive group runs in step on q0's own table and stores nothing)
+// exists; an inactive group runs in step on q0's own table and stores nothing).  Dispatch indices:
+// the table each one prices is xcd_table's
 __device__ __forceinline__ int64_t ahead_table(const PriceArgs& A, int64_t q0, int64_t nblocks,
                                                int lane, bool& act) {
     const int64_t qa = q0 + (int64_t)((lane >> 3) + 1) * A.ahead_stride;
@@ -723,15 +751,16 @@ __device__ __forceinline__ int64_t ahead_table(const PriceArgs& A, int64_t q0, i
 }
 
 // The writer (a first-round block's cut wave, during the CF loop, which leaves it idle on C3's
-// tables): tables q0 + (j + 1) R, j = lane / 8, values 0 .. 7 of the record and K_cf (value 8)
-// into ahead[], then its stores drained (the flags follow the block's CF barrier)
-__device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead& H, int64_t q0,
-                                            int64_t nblocks, int lane) {
+// tables): for the tables of dispatch indices q0 + (j + 1) R, j = lane / 8, the record's 8 values
+// into ahead[], then its stores drained (the flags, which carry K_cf -- returned on sub-lane 0 --
+// follow the block's CF barrier)
+__device__ __forceinline__ int ahead_write(const PriceArgs& A, const FusedHead& H, int64_t q0,
+                                           int64_t nblocks, int lane) {
 #pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
     const int sub = lane & 7;
     bool act;
-    const int64_t q = ahead_table(A, q0, nblocks, lane, act);
-    const int64_t qa = q;
+    const int64_t qa = ahead_table(A, q0, nblocks, lane, act);
+    const int64_t q = xcd_table(A, H.tpp, qa);
     const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
     const int g = (int)((unsigned)q % (unsigned)H.tpp);
     const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
@@ -747,25 +776,13 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
     const double h = A.L * sqrt(fabs(c2));
     const double a = c1 - h;                       // trunc_unclamped (double_heston.py:120-132)
     const double b = c1 + h;
-    const dh::FactorC Fj = dh::factor_consts(v0, k, th, sg, rh);
     const int e_lane = sub < 6 ? sub : 0;
     const double arg = e_lane == 0 ? b : e_lane == 1 ? a : e_lane == 2 ? a + 0.1
                      : e_lane == 3 ? b - 0.1 : e_lane == 4 ? P.muj + 0.5 * (P.sj * P.sj)
                      : -P.r * T;
     const double e = exp(arg);
-    dh::CfConsts CC;
-    double* f1 = (double*)&CC.f1;
-    double* f2 = (double*)&CC.f2;
-    const double* fj = (const double*)&Fj;
-    for (int i = 0; i < (int)(sizeof(dh::FactorC) / 8); ++i) {
-        f1[i] = grp8_bcast(fj[i], 0);
-        f2[i] = grp8_bcast(fj[i], 1);
-    }
     const double comp = grp8_bcast(e, 4) - 1.0;    // cf_consts
-    CC.drift = (P.r - P.q - P.lam * comp) * T;
-    CC.half_sj2 = 0.5 * (P.sj * P.sj);
-    CC.muj = P.muj;
-    CC.lt = P.lam * T;
+    const double drift = (P.r - P.q - P.lam * comp) * T;
     // record value sub of the group's table: a, b, e^b, e^a, slot 25, slot 26, e^{-rT}, drift.
     // The shuffles run on every lane, outside the selection: a lane shuffle inside a branch would
     // read the branch's inactive lanes (sub-lanes 0 and 1 hold e^b and e^a)
@@ -774,26 +791,26 @@ __device__ __forceinline__ void ahead_write(const PriceArgs& A, const FusedHead&
     double v = sub == 0 ? a : sub == 1 ? b : es;
     v = sub == 4 ? e2 * (1.0 + kClampMargin) : v;
     v = sub == 5 ? e3 * (1.0 - kClampMargin) : v;
-    v = sub == 7 ? CC.drift : v;
+    v = sub == 7 ? drift : v;
     if (act) agent_store(A.ahead + qa * kAheadRec + sub, v);
     // K_cf of the group's table by cf_cut_group8 on the same operands (the same first passing
     // candidate as the wave's ballot), then every store of the wave drained
     const int kcf = A.N < kCfCutMinN
                         ? A.N
                         : cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, sub);
-    if (act && sub == 0) agent_store(A.ahead + qa * kAheadRec + 8, kcf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return kcf;
 }
 
-// The reader (wave 0 of a later block whose flag is set): the record's values and the slots
-// re-formed from the parameters, into c[0 .. 30) -- table_prologue_wave's expressions on the
-// same operands, uncontracted, so the same bits
+// The reader (wave 0 of a later block whose flag holds this launch's epoch): the record of dispatch
+// index q and table qt's cheap slots re-formed from the parameters, into c[0 .. 30) --
+// table_prologue_wave's expressions on the same operands, uncontracted, so the same bits
 __device__ __forceinline__ void ahead_read(const PriceArgs& A, const FusedHead& H, int64_t q,
-                                           double* c, int lane) {
+                                           int64_t qt, double* c, int lane) {
 #pragma clang fp contract(off)   // table_prologue and table_prologue_wave: same bits
-    const double v = agent_load(A.ahead + q * kAheadRec + (lane < 8 ? lane : 0));
-    const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
-    const int g = (int)((unsigned)q % (unsigned)H.tpp);
+    const double v = agent_load(A.ahead + q * kAheadRec + (lane & 7));
+    const int64_t p = (int64_t)((unsigned)qt / (unsigned)H.tpp);
+    const int g = (int)((unsigned)qt % (unsigned)H.tpp);
     const Params P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
     const double T = H.tsrc[H.paired ? p : g];
     int2 gr = make_int2((int)p, 1);
@@ -834,21 +851,26 @@ __device__ __forceinline__ void ahead_read(const PriceArgs& A, const FusedHead& 
     }
 }
 
-// The flags, after the writer's stores drained and a barrier (every lane of a wave calls this)
+// The flags, after the writer's stores drained and a barrier (every lane of a wave calls this;
+// kcf: ahead_write's value, read on sub-lane 0)
 __device__ __forceinline__ void ahead_publish(const PriceArgs& A, int64_t q0, int64_t nblocks,
-                                              int lane) {
+                                              int lane, int kcf) {
     bool act;
     const int64_t qa = ahead_table(A, q0, nblocks, lane, act);
     if ((lane & 7) == 0 && act)
-        __hip_atomic_store(&A.ahead_flag[qa], A.ahead_epoch, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&A.ahead_flag[qa],
+                           ((unsigned long long)A.ahead_epoch << 32) | (unsigned)kcf,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The reader: this launch's constants of table q are in ahead[] (a wave-uniform answer)
-__device__ __forceinline__ bool ahead_ready(const PriceArgs& A, int64_t q) {
-    const unsigned f = __hip_atomic_load(&A.ahead_flag[q], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_amdgcn_readfirstlane(f) == A.ahead_epoch;
+// The reader: this launch's record of dispatch index q is in ahead[] (a wave-uniform answer), with
+// its K_cf
+__device__ __forceinline__ bool ahead_ready(const PriceArgs& A, int64_t q, int& kcf) {
+    const unsigned long long f = __hip_atomic_load(&A.ahead_flag[q], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(f >> 32));
+    kcf = (int)__builtin_amdgcn_readfirstlane((unsigned)f);
+    return hi == A.ahead_epoch;
 }
 
 
@@ -1255,6 +1277,65 @@ __device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int 
     }
 }
 
+// Loss pairs handed over inside a multi-round fused launch (partials_only == 3): the
+// guide's data-tagged granule form (cdna_hip_programming.md, Guideline 16 R2; MI355X_MICROARCH.md
+// "valid forms"): every byte of a granule goes out in ONE aligned 8-byte write-through (sc1)
+// store that carries the launch's epoch, and every read of it is an sc1 load, re-read until the
+// tag matches -- no flag, no fence, no drain.  Granule 0 of a task: epoch << 32 | low word of the
+// partial; granule 1: (epoch << 9 | invalid count) << 32 | high word.  The epoch is never 0 and
+// the buffer is zeroed when allocated, so a granule from another launch never matches.
+constexpr int kGranCountBits = 9;           // invalid count of a tile: <= kTileMax = 256
+__device__ __forceinline__ void gran_store(unsigned long long* g, unsigned long long v) {
+    __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long gran_load(const unsigned long long* g) {
+    return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The loss sums of param set pc by one wave of one of the grid's last P blocks (dispatch order),
+// after its own task's granules went out: every lane sweeps its tiles' granules until all carry
+// this launch's epoch (the producers are earlier-dispatched blocks, or blocks of the last round
+// running beside it; at most P waiting blocks of a grid larger than one round of resident ones,
+// so every producer still gets a slot), then the partials are summed in loss_partials_kernel's
+// order and butterfly (same bits as the hand-off's last task).  The sweep is bounded: a timeout
+// (never seen; some 10^8 cycles) leaves n_bad[pc] = -1.
+__device__ __forceinline__ void tail_sums(const PriceArgs& A, int64_t pc, int t) {
+    const int64_t base = pc * A.n_tiles;
+    const unsigned ep = A.ahead_epoch;
+    const unsigned ep_hi = ep << kGranCountBits;
+    const unsigned cmask = (1u << kGranCountBits) - 1u;
+    double acc = 0.0, bad = 0.0;
+    bool timed_out = false;
+    for (int j0 = 0; j0 < A.n_tiles; j0 += 64) {
+        const int j = j0 + t;
+        unsigned long long g0 = 0, g1 = 0;
+        bool ok = j >= A.n_tiles;
+        for (unsigned spins = 0;; ++spins) {
+            if (!ok) {
+                g0 = gran_load(A.gran + 2 * (base + j));
+                g1 = gran_load(A.gran + 2 * (base + j) + 1);
+                ok = (unsigned)(g0 >> 32) == ep && ((unsigned)(g1 >> 32) & ~cmask) == (ep_hi & ~cmask);
+            }
+            if (__all(ok)) break;
+            if (spins > (1u << 20)) {
+                timed_out = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (j < A.n_tiles) {
+            acc += __longlong_as_double((long long)((g1 << 32) | (g0 & 0xffffffffull)));
+            bad += (double)((unsigned)(g1 >> 32) & cmask);
+        }
+    }
+    acc = xor_sum(acc, 64);
+    bad = xor_sum(bad, 64);
+    if (t == 0) {
+        A.sse[pc] = acc;
+        A.n_bad[pc] = timed_out ? -1 : (int)bad;
+    }
+}
+
 // Fixed-order loss partial of one task (wave 0 of the task).  Hand-off to the last task of param
 // set p without fences (MI355X_MICROARCH.md, "Valid forms", first table row): one lane writes
 // the partial with agent-scope (sc1, write-through) stores, drains them with s_waitcnt vmcnt(0),
@@ -1279,6 +1360,18 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     const double f = nb;
     DH_STAMP(A, 14);
     const int64_t base_i = p * A.n_tiles;
+    if (A.partials_only == 3) {     // the pair as two epoch-tagged 8-byte granules, write-through
+        // (agent-scope) stores with no drain: each granule is its own flag (tail_sums)
+        if (t == 0) {
+            const unsigned long long sb = (unsigned long long)__double_as_longlong(s);
+            const unsigned ep = A.ahead_epoch;
+            gran_store(A.gran + 2 * task, ((unsigned long long)ep << 32) | (unsigned)sb);
+            gran_store(A.gran + 2 * task + 1,
+                       ((unsigned long long)((ep << kGranCountBits) | (unsigned)nb) << 32) |
+                           (unsigned)(sb >> 32));
+        }
+        return;
+    }
     if (A.partials_only == 2) {     // one plain 16-byte store (one line write per block):
         // loss_partials_kernel reads the (partial, invalid count) pairs next
         if (t == 0) reinterpret_cast<double2*>(A.part_sse)[task] = make_double2(s, f);
@@ -2087,9 +2180,10 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wv = t >> 6;
-    const int64_t q = blockIdx.x;
-    const int64_t p = (int64_t)(blockIdx.x / (unsigned)H.tpp);    // 32-bit: grids < 2^31 blocks
-    const int g = (int)(blockIdx.x % (unsigned)H.tpp);
+    const int64_t q = blockIdx.x;                       // dispatch index
+    const int64_t qt = xcd_table(A, H.tpp, q);          // the table it prices
+    const int64_t p = (int64_t)((unsigned)qt / (unsigned)H.tpp);   // 32-bit: grids < 2^31 blocks
+    const int g = (int)((unsigned)qt % (unsigned)H.tpp);
     DH_RT_BEGIN(A);
     DH_STAMP(A, 0);
 
@@ -2109,21 +2203,23 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     const int64_t nblocks = gridDim.x;
     if (!H.pre && (wv == 0 || wv == wcut)) serial_prio(true);
     if (H.pre) {
-        if (t < kTabC) shc[t] = H.pre[q * kTabC + t];
+        if (t < kTabC) shc[t] = H.pre[qt * kTabC + t];
     } else if (wv == 0) {
         // (each of the two waves decides on its own flag load and fills its own slots: loaded or
         // formed, the same values, so a flag set between the two loads changes nothing)
-        if (ahead_r && ahead_ready(A, q)) {
-            ahead_read(A, H, q, shc, lane);
-            if (wcut == 0 && lane == 0) shc[30] = agent_load(A.ahead + q * kAheadRec + 8);
+        int kcf_f = 0;
+        if (ahead_r && ahead_ready(A, q, kcf_f)) {
+            ahead_read(A, H, q, qt, shc, lane);
+            if (wcut == 0 && lane == 0) shc[30] = kcf_f;
         } else {
-            table_prologue_wave(A, H, q, shc, lane, wcut == 0);
+            table_prologue_wave(A, H, qt, shc, lane, wcut == 0);
         }
     } else if (wv == wcut) {
-        if (ahead_r && ahead_ready(A, q)) {
-            if (lane == 0) shc[30] = agent_load(A.ahead + q * kAheadRec + 8);
+        int kcf_f = 0;
+        if (ahead_r && ahead_ready(A, q, kcf_f)) {
+            if (lane == 0) shc[30] = kcf_f;
         } else {
-            const int kcf = A.N < kCfCutMinN ? A.N : prologue_cut_wave(A, H, q, lane);
+            const int kcf = A.N < kCfCutMinN ? A.N : prologue_cut_wave(A, H, qt, lane);
             if (lane == 0) shc[30] = kcf;
         }
     }
@@ -2153,7 +2249,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         L.K[i] = K;
         L.mkt[i] = A.mkt ? A.mkt[m] : 0.0;
         L.call[i] = A.call[m];
-        L.perm[i] = A.perm[m];
+        if (A.out) L.perm[i] = A.perm[m];                 // loss requests: no price columns
         L.xK[i] = xK;
         L.exK[i] = ratio;
     }
@@ -2245,13 +2341,14 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     }
     // prologues ahead: the later tables' K_cf on the cut wave; both writer waves' stores drained
     // before the barrier, the flags after it
-    if (ahead_w && wv == wcut) ahead_write(A, H, q, nblocks, lane);
+    int kcf_ahead = 0;
+    if (ahead_w && wv == wcut) kcf_ahead = ahead_write(A, H, q, nblocks, lane);
     if constexpr (!kEarlyClamp) clamp_scan(wv * 64, nthr);
     DH_STAMP(A, 21);
     DH_STAMP_T(A, 22, 64);
     __syncthreads();
     DH_STAMP(A, 2);
-    if (ahead_w && wv == wcut) ahead_publish(A, q, nblocks, lane);
+    if (ahead_w && wv == wcut) ahead_publish(A, q, nblocks, lane, kcf_ahead);
 
     // ---- k-sums in the canonical order of a 64-thread table slot (from the LDS table; the same
     //      bits as cos_table_kernel).  c1 is a sum of zeros (+0.0) and w0 has one nonzero term
@@ -2324,6 +2421,8 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
         if (t < 64) {
             serial_prio(true);
             task_loss(A, p, A.paired ? p : p * A.n_tiles + g, gn, t, L.sse, L.bad);
+            // the grid's last P blocks (dispatch order) then sum one param set each
+            if (A.partials_only == 3 && q >= nblocks - A.P) tail_sums(A, q - (nblocks - A.P), t);
         }
     }
     DH_STAMP(A, 5);
@@ -2625,6 +2724,9 @@ struct dh_ctx {
     // fused kernel builds it applies to, by (t1, r1, LDS bytes)
     DevBuf ahead, ahead_flag;
     size_t ahead_flag_cap = 0;
+    DevBuf gran;               // tail_sums' granules (partials_only == 3), zeroed on allocation
+    size_t gran_cap = 0;
+    int remap_on = -1;         // $DHCOS_XCD_REMAP: fused grids map blocks to tables by XCD (xcd_table)
     unsigned ahead_epoch = 0;
     int ahead_on = -1;
     // the host copy of the next fused launch's param records (dh_surface_fg_begin sets it
@@ -2640,7 +2742,8 @@ struct dh_ctx {
     bool kp_done_set = false;
     int ext_on = -1;
     int defer_on = -1;         // $DHCOS_DEFER: multi-round fused loss requests sum their partials
-                               // in loss_partials_kernel (-1: not read yet)
+                               // in the launch's tail (2), in loss_partials_kernel (1) or through
+                               // the ticket hand-off (0); -1: not read yet
     std::vector<std::pair<std::array<int64_t, 3>, int>> resident_fused;
     GenBufs* gen = nullptr;    // the generator's device draw (dh_gen_device)
 };
@@ -2822,6 +2925,15 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     A.ahead = nullptr;
     A.ahead_flag = nullptr;
     A.ahead_stride = 0;
+    A.gran = nullptr;
+    if (ctx->remap_on < 0) {
+        const char* e = std::getenv("DHCOS_XCD_REMAP");
+        ctx->remap_on = (e && e[0] == '0') ? 0 : 1;
+    }
+    // by XCD: one-round grids of more than one maturity group (below); multi-round grids (C3)
+    // measured slower with it (57.7 vs 56.5 us per request), one-round C2 0.15 us faster
+    A.remap = 0;
+    bool remap_ok = ctx->remap_on && !A.paired && tpp > 1;
     if (ctx->ahead_on < 0) {
         const char* e = std::getenv("DHCOS_AHEAD");
         ctx->ahead_on = (e && e[0] == '0') ? 0 : 1;
@@ -2853,26 +2965,40 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         if (blocks > res) {
             HIP_TRY(ctx->ahead.reserve((size_t)blocks * kAheadRec * sizeof(double)));
             if ((size_t)blocks > ctx->ahead_flag_cap) {
-                HIP_TRY(ctx->ahead_flag.reserve((size_t)blocks * sizeof(unsigned)));
+                HIP_TRY(ctx->ahead_flag.reserve((size_t)blocks * sizeof(unsigned long long)));
                 HIP_TRY(hipMemsetAsync(ctx->ahead_flag.ptr, 0, ctx->ahead_flag.cap, st));
-                ctx->ahead_flag_cap = ctx->ahead_flag.cap / sizeof(unsigned);
+                ctx->ahead_flag_cap = ctx->ahead_flag.cap / sizeof(unsigned long long);
             }
             if (++ctx->ahead_epoch == 0) ++ctx->ahead_epoch;     // 0: the cleared flags' value
             A.ahead = (double*)ctx->ahead.ptr;
-            A.ahead_flag = (unsigned*)ctx->ahead_flag.ptr;
+            A.ahead_flag = (unsigned long long*)ctx->ahead_flag.ptr;
             A.ahead_stride = res;
             A.ahead_epoch = ctx->ahead_epoch;
-            // and the loss sums in a launch of their own (loss_partials_kernel)
+            // and the loss sums deferred: $DHCOS_DEFER = 0 the hand-off's ticket in every block,
+            // 1 loss_partials_kernel after the launch, 2 (default) tail_sums in the launch
             if (ctx->defer_on < 0) {
                 const char* e = std::getenv("DHCOS_DEFER");
-                ctx->defer_on = (e && e[0] == '0') ? 0 : 1;
+                ctx->defer_on = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
             }
-            if (ctx->defer_on && A.part_sse && !A.partials_only && !A.paired) {
+            const int64_t tasks = A.P * A.n_tiles;
+            if (ctx->defer_on == 2 && A.part_sse && !A.partials_only && !A.paired &&
+                A.P <= res / 4 && A.max_group < (1 << kGranCountBits)) {
+                // two granules per task, zeroed when (re)allocated (no epoch is 0)
+                if ((size_t)tasks > ctx->gran_cap) {
+                    HIP_TRY(ctx->gran.reserve((size_t)tasks * 2 * sizeof(unsigned long long)));
+                    HIP_TRY(hipMemsetAsync(ctx->gran.ptr, 0, ctx->gran.cap, st));
+                    ctx->gran_cap = ctx->gran.cap / (2 * sizeof(unsigned long long));
+                }
+                A.gran = (unsigned long long*)ctx->gran.ptr;
+                A.partials_only = 3;
+            } else if (ctx->defer_on && A.part_sse && !A.partials_only && !A.paired) {
                 // (partial, invalid count) pairs: 16 bytes per task
-                HIP_TRY(ctx->part_sse.reserve((size_t)A.P * A.n_tiles * 2 * sizeof(double)));
+                HIP_TRY(ctx->part_sse.reserve((size_t)tasks * 2 * sizeof(double)));
                 A.part_sse = (double*)ctx->part_sse.ptr;
                 A.partials_only = 2;
             }
+        } else if (remap_ok) {
+            A.remap = 1;                         // one round of resident blocks
         }
     }
     if (blocks >= kPrologueKernelMinBlocks && !ctx->stamps_on) {
