@@ -2962,6 +2962,11 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
             res = std::max(1, per_cu) * std::max(1, cus);
             ctx->resident_fused.push_back({key, res});
         }
+        if (ctx->defer_on < 0) {
+            const char* e = std::getenv("DHCOS_DEFER");
+            ctx->defer_on = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
+        }
+        const int defer = ctx->defer_on;
         if (blocks > res) {
             HIP_TRY(ctx->ahead.reserve((size_t)blocks * kAheadRec * sizeof(double)));
             if ((size_t)blocks > ctx->ahead_flag_cap) {
@@ -2974,31 +2979,31 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
             A.ahead_flag = (unsigned long long*)ctx->ahead_flag.ptr;
             A.ahead_stride = res;
             A.ahead_epoch = ctx->ahead_epoch;
-            // and the loss sums deferred: $DHCOS_DEFER = 0 the hand-off's ticket in every block,
-            // 1 loss_partials_kernel after the launch, 2 (default) tail_sums in the launch
-            if (ctx->defer_on < 0) {
-                const char* e = std::getenv("DHCOS_DEFER");
-                ctx->defer_on = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
-            }
-            const int64_t tasks = A.P * A.n_tiles;
-            if (ctx->defer_on == 2 && A.part_sse && !A.partials_only && !A.paired &&
-                A.P <= res / 4 && A.max_group < (1 << kGranCountBits)) {
-                // two granules per task, zeroed when (re)allocated (no epoch is 0)
-                if ((size_t)tasks > ctx->gran_cap) {
-                    HIP_TRY(ctx->gran.reserve((size_t)tasks * 2 * sizeof(unsigned long long)));
-                    HIP_TRY(hipMemsetAsync(ctx->gran.ptr, 0, ctx->gran.cap, st));
-                    ctx->gran_cap = ctx->gran.cap / (2 * sizeof(unsigned long long));
-                }
-                A.gran = (unsigned long long*)ctx->gran.ptr;
-                A.partials_only = 3;
-            } else if (ctx->defer_on && A.part_sse && !A.partials_only && !A.paired) {
+            // and the loss sums deferred (below), or in loss_partials_kernel ($DHCOS_DEFER=1)
+            if (defer == 1 && A.part_sse && !A.partials_only && !A.paired) {
                 // (partial, invalid count) pairs: 16 bytes per task
-                HIP_TRY(ctx->part_sse.reserve((size_t)tasks * 2 * sizeof(double)));
+                HIP_TRY(ctx->part_sse.reserve((size_t)A.P * A.n_tiles * 2 * sizeof(double)));
                 A.part_sse = (double*)ctx->part_sse.ptr;
                 A.partials_only = 2;
             }
         } else if (remap_ok) {
             A.remap = 1;                         // one round of resident blocks
+        }
+        // loss sums in the launch's tail ($DHCOS_DEFER=2, the default; 0: the hand-off's ticket in
+        // every block): C3 -1.1 us against loss_partials_kernel, C2 (one round) -0.5 us against
+        // the ticket.  At most a quarter of the resident blocks wait (tail_sums)
+        if (defer == 2 && A.part_sse && !A.partials_only && !A.paired && A.P <= res / 4 &&
+            A.max_group < (1 << kGranCountBits)) {
+            if (A.ahead_stride == 0 && ++ctx->ahead_epoch == 0) ++ctx->ahead_epoch;
+            A.ahead_epoch = ctx->ahead_epoch;
+            const int64_t tasks = A.P * A.n_tiles;
+            if ((size_t)tasks > ctx->gran_cap) {    // two granules per task, zeroed (no epoch is 0)
+                HIP_TRY(ctx->gran.reserve((size_t)tasks * 2 * sizeof(unsigned long long)));
+                HIP_TRY(hipMemsetAsync(ctx->gran.ptr, 0, ctx->gran.cap, st));
+                ctx->gran_cap = ctx->gran.cap / (2 * sizeof(unsigned long long));
+            }
+            A.gran = (unsigned long long*)ctx->gran.ptr;
+            A.partials_only = 3;
         }
     }
     if (blocks >= kPrologueKernelMinBlocks && !ctx->stamps_on) {
