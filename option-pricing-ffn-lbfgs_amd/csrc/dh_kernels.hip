@@ -133,7 +133,8 @@ struct PriceArgs {
     // partials_only == 3: [P * n_tiles][2] granules (epoch-tagged halves of each task's pair)
     unsigned long long* gran;
     int remap;              // fused kernel: dispatch index -> table by XCD (xcd_table), else 0
-    int unused_pad;
+    int host_out;           // sse / n_bad in mapped host memory (the host API's zero-copy
+                            // requests): written by system-scope stores, drained (loss_out)
 };
 
 // w_k of table q sits at table_w(A, q)[k * table_step(A)].  The small-tile option kernel has one
@@ -749,7 +750,6 @@ __device__ __forceinline__ int64_t ahead_table(const PriceArgs& A, int64_t q0, i
     act = qa < nblocks;
     return act ? qa : q0;
 }
-
 // The writer (a first-round block's cut wave, during the CF loop, which leaves it idle on C3's
 // tables): for the tables of dispatch indices q0 + (j + 1) R, j = lane / 8, the record's 8 values
 // into ahead[], then its stores drained (the flags, which carry K_cf -- returned on sub-lane 0 --
@@ -1277,19 +1277,45 @@ __device__ __forceinline__ void record_price(const PriceArgs& A, int64_t p, int 
     }
 }
 
-// Loss pairs handed over inside a multi-round fused launch (partials_only == 3): the
-// guide's data-tagged granule form (cdna_hip_programming.md, Guideline 16 R2; MI355X_MICROARCH.md
-// "valid forms"): every byte of a granule goes out in ONE aligned 8-byte write-through (sc1)
-// store that carries the launch's epoch, and every read of it is an sc1 load, re-read until the
-// tag matches -- no flag, no fence, no drain.  Granule 0 of a task: epoch << 32 | low word of the
+// Loss pairs handed over inside a fused launch (partials_only == 3): the guide's data-tagged
+// granule form (cdna_hip_programming.md, Guideline 16 R2; MI355X_MICROARCH.md "valid forms"):
+// every byte of a granule goes out in one aligned write-through (sc1) store that carries the
+// launch's epoch, and every read of it is an sc1 load, re-read until the tag matches -- no flag,
+// no fence, no drain.  Granule 0 of a task: epoch << 32 | low word of the
 // partial; granule 1: (epoch << 9 | invalid count) << 32 | high word.  The epoch is never 0 and
 // the buffer is zeroed when allocated, so a granule from another launch never matches.
 constexpr int kGranCountBits = 9;           // invalid count of a tile: <= kTileMax = 256
-__device__ __forceinline__ void gran_store(unsigned long long* g, unsigned long long v) {
-    __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ unsigned long long gran_load(const unsigned long long* g) {
     return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// A task's two granules in ONE 16-byte write-through store (buffer_store_dwordx4 with sc1: aux 16,
+// cdna_hip_programming.md Guideline 16 R1's store form), one fabric write instead of two; each
+// 8-byte half still carries its own tag, so a torn pair is seen as not yet written.  g: uniform.
+typedef unsigned int dh_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void gran_store2(unsigned long long* g, unsigned long long v0,
+                                            unsigned long long v1) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(g, 0, 16, 0x00020000);
+    const dh_u32x4 d = {(unsigned)v0, (unsigned)(v0 >> 32), (unsigned)v1, (unsigned)(v1 >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(d, rsrc, 0, 0, 16);
+}
+
+// The final sse / n_bad of param set p (lane 0 of the summing wave).  Into mapped host memory
+// (host_out) they go as system-scope stores and the wave waits for their acknowledgement before it
+// ends, so they are complete before the kernel's end-of-dispatch signal, whichever release scope
+// the runtime gives that signal (the slot's event may be the launch's own stop event,
+// hipExtLaunchKernel, whose release scope HIP does not document).
+#ifndef DH_HOST_OUT_DRAIN
+#define DH_HOST_OUT_DRAIN 1
+#endif
+__device__ __forceinline__ void loss_out(const PriceArgs& A, int64_t p, double sse, int nb) {
+    if (DH_HOST_OUT_DRAIN && A.host_out) {
+        __hip_atomic_store(&A.sse[p], sse, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&A.n_bad[p], nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        A.sse[p] = sse;
+        A.n_bad[p] = nb;
+    }
 }
 
 // The loss sums of param set pc by one wave of one of the grid's last P blocks (dispatch order),
@@ -1330,10 +1356,7 @@ __device__ __forceinline__ void tail_sums(const PriceArgs& A, int64_t pc, int t)
     }
     acc = xor_sum(acc, 64);
     bad = xor_sum(bad, 64);
-    if (t == 0) {
-        A.sse[pc] = acc;
-        A.n_bad[pc] = timed_out ? -1 : (int)bad;
-    }
+    if (t == 0) loss_out(A, pc, acc, timed_out ? -1 : (int)bad);
 }
 
 // Fixed-order loss partial of one task (wave 0 of the task).  Hand-off to the last task of param
@@ -1365,10 +1388,10 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
         if (t == 0) {
             const unsigned long long sb = (unsigned long long)__double_as_longlong(s);
             const unsigned ep = A.ahead_epoch;
-            gran_store(A.gran + 2 * task, ((unsigned long long)ep << 32) | (unsigned)sb);
-            gran_store(A.gran + 2 * task + 1,
-                       ((unsigned long long)((ep << kGranCountBits) | (unsigned)nb) << 32) |
-                           (unsigned)(sb >> 32));
+            const unsigned long long g0 = ((unsigned long long)ep << 32) | (unsigned)sb;
+            const unsigned long long g1 =
+                ((unsigned long long)((ep << kGranCountBits) | (unsigned)nb) << 32) | (unsigned)(sb >> 32);
+            gran_store2(A.gran + 2 * task, g0, g1);
         }
         return;
     }
@@ -1402,8 +1425,7 @@ __device__ __forceinline__ void task_loss(const PriceArgs& A, int64_t p, int64_t
     acc = xor_sum(acc, 64);
     bad = xor_sum(bad, 64);
     if (t == 0) {
-        A.sse[p] = acc;
-        A.n_bad[p] = (int)bad;
+        loss_out(A, p, acc, (int)bad);
         __hip_atomic_store(&A.counter[p * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -1531,8 +1553,13 @@ __device__ __forceinline__ void tile_sums_r(const PriceArgs& A, int64_t p, const
         if (pass == 0) DH_STAMP(A, 10);
         if (lds_red) {
             if (gvalid) {
+                // the slot address formed here, not kept across the angle loop (held there, it was
+                // the C3 build's one hot-path register spill: a scratch store and a reload per
+                // thread, ~1.3 MB of scratch written back per request)
+                int tr = t;
+                asm volatile("" : "+v"(tr));
 #pragma unroll
-                for (int j = 0; j < RT; ++j) red[j * kBlock + t] = sm[j];
+                for (int j = 0; j < RT; ++j) red[j * kBlock + tr] = sm[j];
             }
             __syncthreads();
             if (pass == 0) DH_STAMP(A, 11);
@@ -1891,8 +1918,7 @@ __global__ __launch_bounds__(kBlock) void cos_option_small_kernel(PriceArgs A_, 
         acc += __hip_atomic_load(&A.part_sse[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bad += __hip_atomic_load(&A.part_bad[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    A.sse[p] = acc;
-    A.n_bad[p] = bad;
+    loss_out(A, p, acc, bad);
     __hip_atomic_store(&A.counter[p * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2136,8 +2162,7 @@ __global__ __launch_bounds__(kBlock, 3) void cos_gen_kernel(PriceArgs A_, int OP
                         s2 += __hip_atomic_load(&A.part_sse[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         bad += __hip_atomic_load(&A.part_bad[base_i + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    A.sse[pp] = s2;
-                    A.n_bad[pp] = bad;
+                    loss_out(A, pp, s2, bad);
                     __hip_atomic_store(&A.counter[pp * kCounterStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
@@ -2968,9 +2993,10 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         }
         const int defer = ctx->defer_on;
         if (blocks > res) {
-            HIP_TRY(ctx->ahead.reserve((size_t)blocks * kAheadRec * sizeof(double)));
-            if ((size_t)blocks > ctx->ahead_flag_cap) {
-                HIP_TRY(ctx->ahead_flag.reserve((size_t)blocks * sizeof(unsigned long long)));
+            const size_t slots = (size_t)blocks;
+            HIP_TRY(ctx->ahead.reserve(slots * kAheadRec * sizeof(double)));
+            if (slots > ctx->ahead_flag_cap) {
+                HIP_TRY(ctx->ahead_flag.reserve(slots * sizeof(unsigned long long)));
                 HIP_TRY(hipMemsetAsync(ctx->ahead_flag.ptr, 0, ctx->ahead_flag.cap, st));
                 ctx->ahead_flag_cap = ctx->ahead_flag.cap / sizeof(unsigned long long);
             }
@@ -3535,6 +3561,7 @@ static int surface_loss_launch(dh_ctx* ctx, const dh_surface* s, const double* d
     A.n_bad = (int*)d_n_bad;
     A.live_count = live_count;
     A.partials_only = partials_only && !A.exact ? 1 : 0;
+    A.host_out = ctx->kp_src != nullptr;     // the host API's zero-copy requests (kp_src set)
     return launch_price(ctx, A, st);
 }
 
