@@ -22,5 +22,6 @@ fi
 
 # the per-dispatch traces are not needed by summarize_profiles.py and would pass the 64 MiB merge cap
 gzip -f gpurun_out/prof/${TAG}_default_cmd_kernel_trace.csv 2>/dev/null; rm -f gpurun_out/prof/*_kernel_trace.csv
+gzip -f gpurun_out/prof/*_counter_collection.csv 2>/dev/null
 du -sh gpurun_out
 echo done

@@ -18,6 +18,7 @@ import argparse
 import collections
 import csv
 import glob
+import gzip
 import json
 import os
 import shutil
@@ -92,8 +93,9 @@ def main():
                       key=lambda k: total[k])
             req_kernels = ("cos_table_kernel", opt)
         vals = collections.defaultdict(list)
-        for f in glob.glob(os.path.join(args.src, f"{args.tag}_{c}_pmc*_counter_collection.csv")):
-            for r in csv.DictReader(open(f)):
+        for f in glob.glob(os.path.join(args.src, f"{args.tag}_{c}_pmc*_counter_collection.csv*")):
+            fh = gzip.open(f, "rt") if f.endswith(".gz") else open(f)
+            for r in csv.DictReader(fh):
                 k = short(r["Kernel_Name"])
                 if k:
                     vals[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
@@ -109,8 +111,19 @@ def main():
             write = med.get((k, "WRITE_SIZE"))
             e = {"avg_ns": avg.get(k)}
             if fetch is not None and write is not None:
-                e["fetch_bytes"] = 2.0 * fetch * 1024.0
+                e["fetch_bytes_x2"] = 2.0 * fetch * 1024.0
+                e["fetch_bytes"] = e["fetch_bytes_x2"]
                 e["write_bytes"] = write * 1024.0
+            sized = [med.get((k, f"TCC_EA0_RDREQ_{b}B_sum")) for b in (32, 64, 128)]
+            if all(x is not None for x in sized):
+                # the L2's memory-side read requests by size: the fetched bytes exactly (the x2
+                # of FETCH_SIZE is calibrated for 16-B-per-lane streaming reads only)
+                e["fetch_bytes"] = 32.0 * sized[0] + 64.0 * sized[1] + 128.0 * sized[2]
+                e["fetch_basis"] = "TCC_EA0_RDREQ_{32,64,128}B x size"
+            for n in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCC_EA0_RDREQ_DRAM_32B_sum",
+                      "TCC_EA0_WRREQ_DRAM_sum", "TCC_EA0_WRREQ_64B_sum"):
+                if (k, n) in med:
+                    e[n] = med[(k, n)]
             f64 = [med.get((k, n)) for n in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
                                              "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")]
             if all(x is not None for x in f64):
@@ -129,7 +142,9 @@ def main():
         req_ns = sum(per_kernel[k]["avg_ns"] or 0.0 for k in req_kernels)
         traffic[c] = {"round": args.tag, "hbm_bytes_per_launch": hbm, "request_avg_ns": req_ns,
                       "kernels": per_kernel,
-                      "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->bytes, the request's kernels"}
+                      "note": "fetched bytes from the L2's read requests by size (32/64/128 B) "
+                              "where collected, else FETCH_SIZE x2 (gfx950); + WRITE_SIZE; the "
+                              "request's kernels"}
         md += [f"## {c}", "", "| kernel | avg us | fetch MB | write MB | exec fp64 GFLOP | "
                "exec fp64 TFLOP/s | wait_any/wave_cycles |", "|---|---|---|---|---|---|---|"]
         for k in req_kernels:
