@@ -549,8 +549,14 @@ static_assert(offsetof(FusedKargs, A) == kFusedArgsKernargOff, "PriceArgs kernar
 // start's 14 records: 1,792 bytes, 2,416 with the rest of the arguments and 2,672 with the
 // runtime's hidden ones (28 records would pass the 4 KiB segment).
 constexpr int kKargSets = 14;
+// and, for surfaces of at most kKargGroups maturity groups (C1's 3, C2's 32), the groups' maturities
+// and option ranges: the prologue's first dependent load (the table's T) then comes from the
+// kernel-argument segment too instead of device memory (C2 prologue chain: one memory round trip)
+constexpr int kKargGroups = 32;
 struct KargParams {
     double v[kKargSets * DH_PARAM_STRIDE];
+    double T[kKargGroups];
+    int2 groups[kKargGroups];
 };
 struct NoKargParams {
     int unused;
@@ -2189,8 +2195,9 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     typename std::conditional<KP, KargParams, NoKargParams>::type pb_) {
     // KP: the records are the param block at the end of the kernel arguments (read in place)
     const double* prm0 = KP ? karg_ref<KargParams, kFusedParamsKernargOff>().v : h_prm;
-    const FusedHead H{prm0, h_tsrc, h_groups, h_live ? h_live : &kLiveOne, h_pre, h_tpp,
-                      h_paired};
+    const double* tsrc0 = KP ? karg_ref<KargParams, kFusedParamsKernargOff>().T : h_tsrc;
+    const int2* groups0 = KP ? karg_ref<KargParams, kFusedParamsKernargOff>().groups : h_groups;
+    const FusedHead H{prm0, tsrc0, groups0, h_live ? h_live : &kLiveOne, h_pre, h_tpp, h_paired};
     const PriceArgs& A = karg_ref<PriceArgs, kFusedArgsKernargOff>();
     // the halt test's load is issued here (a global load: a flat one would also hold up every
     // scalar load's wait) and its value used after the staging barrier, so it overlaps the
@@ -2758,6 +2765,7 @@ struct dh_ctx {
     // around its launch): fused launches of <= kKargSets records pass them in their kernel
     // arguments; $DHCOS_KARG_PARAMS=0 turns that off (kp_on: -1 not read yet)
     const double* kp_src = nullptr;
+    const dh_surface* kp_surf = nullptr;   // and its surface (host copies of the groups)
     int64_t kp_n = 0;
     int kp_on = -1;
     // and its completion event: recorded by the launch itself (hipExtLaunchKernel's stop event)
@@ -2792,6 +2800,8 @@ struct dh_surface {
     double* group_T = nullptr;
     int2* groups = nullptr;
     void* block = nullptr;  // the one device allocation every array above points into
+    std::vector<double> h_group_T;   // host copies of group_T / groups (the fused launch's
+    std::vector<int2> h_groups;      // kernel arguments, KargParams)
 };
 
 namespace {
@@ -3046,10 +3056,14 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
         const char* e = std::getenv("DHCOS_KARG_PARAMS");
         ctx->kp_on = (e && e[0] == '0') ? 0 : 1;
     }
-    if (ctx->kp_on && ctx->kp_src && A.P == ctx->kp_n && A.P <= kKargSets && r1 && !wide &&
+    if (ctx->kp_on && ctx->kp_src && ctx->kp_surf && !A.paired &&
+        (int)ctx->kp_surf->h_group_T.size() == tpp && tpp <= kKargGroups &&
+        A.P == ctx->kp_n && A.P <= kKargSets && r1 && !wide &&
         blocks < kPrologueKernelMinBlocks && !ctx->stamps_on && !A.exact) {
         KargParams pb{};
         std::memcpy(pb.v, ctx->kp_src, (size_t)A.P * DH_PARAM_STRIDE * sizeof(double));
+        std::memcpy(pb.T, ctx->kp_surf->h_group_T.data(), (size_t)tpp * sizeof(double));
+        std::memcpy(pb.groups, ctx->kp_surf->h_groups.data(), (size_t)tpp * sizeof(int2));
         if (ctx->ext_on < 0) {
             const char* e = std::getenv("DHCOS_EXT_EVENT");
             ctx->ext_on = (e && e[0] == '0') ? 0 : 1;
@@ -3425,6 +3439,8 @@ int dh_surface_create(dh_ctx* ctx, const double* K, const double* T, const int8_
     s->max_group = max_group;
     s->strike_mode = strike_mode;
     s->has_mkt = mkt != nullptr;
+    s->h_group_T = group_T;
+    s->h_groups = groups;
     // every array in one device allocation, staged on the host and uploaded by one copy (one
     // hipMalloc and one synchronous copy instead of nine of each: ~0.5 ms of a C3 calibration)
     struct Part {
@@ -3675,11 +3691,13 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
         double* h_sse = (double*)ctx->h_loss.ptr;
         int32_t* h_bad = (int32_t*)(h_sse + S);
         ctx->kp_src = (const double*)ctx->h_params.ptr;     // <= 14 records: in the arguments
+        ctx->kp_surf = s;
         ctx->kp_n = S;
         rc = dh_surface_loss_dev(ctx, s, (const double*)ctx->h_params.dptr, S, N, L,
                                  (double*)ctx->h_loss.dptr, (int32_t*)((double*)ctx->h_loss.dptr + S),
                                  d_prices, ctx->stream);
         ctx->kp_src = nullptr;
+        ctx->kp_surf = nullptr;
         ctx->kp_n = 0;
         if (rc) return rc;
         if (prices && s->M > 0)
@@ -4770,6 +4788,7 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
     fg_points(x0, model, S, S0, r, (double*)F.h_params.ptr, F.pen.data(), F.dx.data());
     // the records also travel in the fused launch's kernel arguments when they fit (KargParams)
     ctx->kp_src = (const double*)F.h_params.ptr;
+    ctx->kp_surf = s;
     ctx->kp_n = (int64_t)P;
     ctx->kp_done = F.done;
     ctx->kp_done_set = false;
@@ -4777,6 +4796,7 @@ extern "C" int dh_surface_fg_begin(dh_ctx* ctx, const dh_surface* s, const doubl
                              (double*)F.h_loss.dptr, (int32_t*)((double*)F.h_loss.dptr + P),
                              nullptr, ctx->stream);
     ctx->kp_src = nullptr;
+    ctx->kp_surf = nullptr;
     ctx->kp_n = 0;
     ctx->kp_done = nullptr;
     if (rc) return rc;
