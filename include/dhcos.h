@@ -124,14 +124,18 @@ int dh_host_unregister(void* ptr);
  *   sse[s]   = sum_m ((price_sm - mkt_m) / mkt_m)^2      (lbfgs_calibrator.py:163, un-normalised)
  *   n_bad[s] = #{m : price_sm is NaN, +-inf or <= 0}      (lbfgs_calibrator.py:152)
  *   prices   = optional [S][M] output (NULL to skip)
- * The host forms loss = n_bad ? 1e10 : sse / M + feller (lbfgs_calibrator.py:118-177).       */
+ * The host forms loss = n_bad ? 1e10 : sse / M + feller (lbfgs_calibrator.py:118-177).
+ * A fused request sums each set's tile partials in its own tail; a sum whose
+ * hand-off never completed (bounded wait, never observed) leaves n_bad[s] = -1 and the call
+ * returns DH_E_HIP.                                                                            */
 int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int S, int N,
                     double L, double* sse, int32_t* n_bad, double* prices);
 
 /* Device-pointer variants: params/out/sse/n_bad are device pointers; enqueue on `stream`
  * (hipStream_t; NULL = context stream).  No synchronisation, no allocation after warm-up.
  * A request is one fused launch or two launches (COS table, then options), dh_ctx_set_path;
- * in loss mode the last task of each param set finalises its sum in a fixed order.
+ * in loss mode each param set's sum is finalised in a fixed order (n_bad[s] = -1: a hand-off
+ * timeout, see dh_surface_loss).
  * Launches through one context share its scratch: issue them on one stream at a time.       */
 int dh_surface_price_dev(dh_ctx* ctx, const dh_surface* s, const double* d_params, int64_t P,
                          int N, double L, double* d_out, void* stream);

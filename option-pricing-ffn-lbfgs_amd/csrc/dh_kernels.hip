@@ -2810,6 +2810,16 @@ namespace {
 // than the fast path's LDS-resident table holds (N > DH_MAX_N).
 bool per_term(const dh_ctx* ctx, int N) { return ctx->exact || N > DH_MAX_N; }
 
+// A negative invalid count is tail_sums' timeout marker (a loss hand-off that never completed):
+// an error, not a loss
+int check_loss_counts(const int32_t* n_bad, int64_t S) {
+    for (int64_t i = 0; i < S; ++i)
+        if (n_bad[i] < 0)
+            return fail(DH_E_HIP, "loss hand-off timed out in the fused kernel (param set " +
+                                      std::to_string(i) + ")");
+    return DH_OK;
+}
+
 // Busy-wait for a short request (a calibration iteration waits on it): polling hipStreamQuery
 // returns as soon as the stream drains, where hipStreamSynchronize may yield the thread.
 int spin_sync(hipStream_t st) {
@@ -3706,7 +3716,7 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
         if (rc) return rc;
         std::memcpy(sse, h_sse, (size_t)S * 8);
         std::memcpy(n_bad, h_bad, (size_t)S * 4);
-        return DH_OK;
+        return check_loss_counts(n_bad, S);
     }
     HIP_TRY(ctx->params.reserve(pb));
     HIP_TRY(ctx->sse.reserve((size_t)S * 8));
@@ -3720,7 +3730,7 @@ int dh_surface_loss(dh_ctx* ctx, const dh_surface* s, const double* params, int 
     if (prices && s->M > 0)
         HIP_TRY(hipMemcpyAsync(prices, d_prices, ob, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    return DH_OK;
+    return check_loss_counts(n_bad, S);
 }
 
 int dh_price_pairs(dh_ctx* ctx, const double* params, const double* K, const double* T,
@@ -4831,8 +4841,10 @@ extern "C" int dh_surface_fg_end(dh_ctx* ctx, const dh_surface* s, int slot, int
         }
     }
     F.pending = false;
-    fg_finish(F.S, F.M, (const double*)F.h_loss.ptr, (const int32_t*)((double*)F.h_loss.ptr + P),
-              F.pen.data(), F.dx.data(), f, g, low);
+    const int32_t* nb = (const int32_t*)((double*)F.h_loss.ptr + P);
+    const int crc = check_loss_counts(nb, (int64_t)P);
+    if (crc) return crc;
+    fg_finish(F.S, F.M, (const double*)F.h_loss.ptr, nb, F.pen.data(), F.dx.data(), f, g, low);
     return DH_OK;
 }
 
