@@ -37,7 +37,8 @@ e_ref > 1e-11; they are counted and printed with both errors (known
 Cases: the C2 iterating start (calibrate(300, 1) from start 1 of calibrate(300, 3) under
 np.random.seed(0), tests/golden/calib_c2_start1.json's x0, 1,024 options, N = 256) -- every
 request of both drivers; C3 (10,000 options, N = 512, the three np.random.seed(0) starts) -- the
-first five requests of every start, both drivers."""
+first five requests of every start, both drivers; C4 (64 starts on the C2 surface) -- the first
+two requests of every start, both drivers."""
 import json
 import os
 from concurrent.futures import ThreadPoolExecutor
@@ -226,4 +227,33 @@ def test_shadow_c3_first_requests(dh, driver):
     for s in range(3):
         assert np.array_equal(next(t[2] for t in first if t[0] == s and t[1] == 0), x0s[s])
     shadow(first, cal._get_surface(), K, T, call, mkt, S0, r, N, f"C3 {driver}",
+           device_transform=driver == "device")
+
+
+@pytest.mark.parametrize("driver", ["scipy", "device"])
+def test_shadow_c4_first_requests(dh, driver):
+    """C4 (configs[3]: 64 starts on the 1,024-option C2 surface, N = 256; its requests run the
+    prologue kernel and the <= 96-VGPR fused build): the first two requests of every one of the 64
+    np.random.seed(0) starts (both drivers) against the reference's objective and FD gradient."""
+    from dhcos import _native
+    S0, r, N = 100.0, 0.03, 256
+    kk, tt = np.meshgrid(np.linspace(0.8, 1.2, 32) * S0, np.linspace(0.1, 2.0, 32))
+    K, T = kk.ravel(), tt.ravel()
+    call = np.ones(K.size, dtype=bool)
+    true = GEN_LO + (GEN_HI - GEN_LO) * np.random.RandomState(1).rand(13)
+    rec = np.zeros((1, 16))
+    rec[0, :13], rec[0, 13], rec[0, 14] = true, S0, r
+    model = _native.Surface(_native.default_context(), K, T, call).price(rec, N)[0]
+    mkt = model * (1 + np.random.RandomState(2).normal(0, 0.02, K.size))
+    opts = [{"strike": float(k), "maturity": float(t), "price": float(p), "option_type": "call"}
+            for k, t, p in zip(K, T, mkt)]
+    np.random.seed(0)
+    cal = dh.DoubleHestonJumpCalibrator(S0, r, opts, N=N)
+    x0s = cal.start_points(64)
+    res, trace = traced_calibration(cal, x0s, driver)
+    first = [t for t in trace if t[1] < 2]
+    assert sorted({t[0] for t in first}) == list(range(64))
+    for s in range(64):
+        assert np.array_equal(next(t[2] for t in first if t[0] == s and t[1] == 0), x0s[s])
+    shadow(first, cal._get_surface(), K, T, call, mkt, S0, r, N, f"C4 {driver}",
            device_transform=driver == "device")
