@@ -2758,7 +2758,8 @@ struct dh_ctx {
     size_t ahead_flag_cap = 0;
     DevBuf gran;               // tail_sums' granules (partials_only == 3), zeroed on allocation
     size_t gran_cap = 0;
-    int remap_on = -1;         // $DHCOS_XCD_REMAP: fused grids map blocks to tables by XCD (xcd_table)
+    int remap_on = -1;         // $DHCOS_XCD_REMAP: one-round fused grids map blocks to tables by XCD
+                               // (xcd_table; 0 off, 2 multi-round grids too)
     unsigned ahead_epoch = 0;
     int ahead_on = -1;
     // the host copy of the next fused launch's param records (dh_surface_fg_begin sets it
@@ -2973,7 +2974,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
     A.gran = nullptr;
     if (ctx->remap_on < 0) {
         const char* e = std::getenv("DHCOS_XCD_REMAP");
-        ctx->remap_on = (e && e[0] == '0') ? 0 : 1;
+        ctx->remap_on = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 1;
     }
     // by XCD: one-round grids of more than one maturity group (below); multi-round grids (C3)
     // measured slower with it (57.7 vs 56.5 us per request), one-round C2 0.15 us faster
@@ -3025,6 +3026,7 @@ int launch_fused(dh_ctx* ctx, const PriceArgs& A0, hipStream_t st) {
             A.ahead_flag = (unsigned long long*)ctx->ahead_flag.ptr;
             A.ahead_stride = res;
             A.ahead_epoch = ctx->ahead_epoch;
+            if (ctx->remap_on == 2 && remap_ok) A.remap = 1;   // C3 +1.1 us: off by default
             // and the loss sums deferred (below), or in loss_partials_kernel ($DHCOS_DEFER=1)
             if (defer == 1 && A.part_sse && !A.partials_only && !A.paired) {
                 // (partial, invalid count) pairs: 16 bytes per task

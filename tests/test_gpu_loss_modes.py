@@ -3,7 +3,7 @@
 A fused loss request sums each param set's tile partials in one of three ways ($DHCOS_DEFER: 2, the
 default, the grid's last blocks from epoch-tagged granules; 1, a summing launch after the grid;
 0, the ticket hand-off in every block), and one-round grids map blocks to tables by XCD
-($DHCOS_XCD_REMAP).  Every form reads the same partials in the same order and butterfly, and the map
+($DHCOS_XCD_REMAP=1, the default; =2 multi-round grids too).  Every form reads the same partials in the same order and butterfly, and the map
 is a bijection, so sse and n_bad must be bit for bit the same -- on a multi-round grid (C3's shape:
 4,200 tables) and a one-round grid (C2's: 448), with an invalid price in the market (n_bad > 0),
 and over back-to-back requests (the granules' epochs).  Each setting gets a context of its own (the
@@ -67,7 +67,8 @@ def test_loss_modes_and_maps_bitwise(native, nK, nT, N):
     assert (want_bad[5] > 0) and (want_bad > 0).sum() >= 1
     for env in ({"DHCOS_DEFER": "1", "DHCOS_XCD_REMAP": "0"},
                 {"DHCOS_DEFER": "2", "DHCOS_XCD_REMAP": "0"},
-                {"DHCOS_DEFER": "2", "DHCOS_XCD_REMAP": "1"}):
+                {"DHCOS_DEFER": "2", "DHCOS_XCD_REMAP": "1"},
+                {"DHCOS_DEFER": "2", "DHCOS_XCD_REMAP": "2"}):    # by XCD on multi-round grids too
         sse, bad = losses(native, env, K, T, call, mkt, recs, N)
         assert np.array_equal(bad, want_bad), env
         assert np.array_equal(sse.view(np.int64), want_sse.view(np.int64)), \
