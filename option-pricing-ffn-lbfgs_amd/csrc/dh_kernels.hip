@@ -570,6 +570,35 @@ constexpr int kFusedParamsKernargOff = 384;
 static_assert(offsetof(FusedKargsKP, pb) == kFusedParamsKernargOff, "param block kernarg offset");
 static_assert(sizeof(FusedKargsKP) + 256 <= 4096, "kernel arguments over 4 KiB");
 
+#ifndef DH_KARG_PREFETCH
+#define DH_KARG_PREFETCH 1
+#endif
+// The kernel-argument lines the fused kernel reads PriceArgs from (in place, karg_ref), pulled
+// into the scalar cache in ONE round trip at entry: one s_load_dword per 64-byte line brings the
+// whole line, and the wave waits once.  Without it the prologue's path met each line as its own
+// dependent round trip (xcd_table's switch, the ahead stride, the tail-cut and table fields: five
+// serial ~550-cycle misses before the table record could be loaded, tools/ubench/kernarg_latency).
+// The lines are 64 bytes apart from byte 0x30 through 0x1b0 (PriceArgs and the arguments after
+// it), so every line is touched whatever the segment's alignment.
+__device__ __forceinline__ void karg_prefetch_lines() {
+#if DH_KARG_PREFETCH
+    const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    unsigned d0, d1, d2, d3, d4, d5, d6;
+    asm volatile(
+        "s_load_dword %0, %7, 0x30\n\t"
+        "s_load_dword %1, %7, 0x70\n\t"
+        "s_load_dword %2, %7, 0xb0\n\t"
+        "s_load_dword %3, %7, 0xf0\n\t"
+        "s_load_dword %4, %7, 0x130\n\t"
+        "s_load_dword %5, %7, 0x170\n\t"
+        "s_load_dword %6, %7, 0x1b0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=s"(d0), "=s"(d1), "=s"(d2), "=s"(d3), "=s"(d4), "=s"(d5), "=s"(d6)
+        : "s"(ka)
+        : "memory");
+#endif
+}
+
 // the live count read by launches without one (FusedHead::live): the halt test is then a load
 // like any other, with no branch on the pointer (a branch made the compiler wait for it at the
 // kernel's entry)
@@ -603,6 +632,10 @@ __device__ __forceinline__ void prologue_range_wave(const PriceArgs& A, const Fu
     const int g = (int)((unsigned)q % (unsigned)H.tpp);
     P = dh::load_params(H.prm + p * DH_PARAM_STRIDE);
     T = H.tsrc[H.paired ? p : g];
+#ifdef DH_STAMPS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the record and T (scalar loads) are in
+#endif
+    DH_STAMP_T(A, 31, 0);
     const bool two = lane & 1;                     // factor 2 on odd lanes
     const double v0 = two ? P.v02 : P.v01, k = two ? P.k2 : P.k1, th = two ? P.t2 : P.t1;
     const double sg = two ? P.s2 : P.s1, rh = two ? P.r2 : P.r1;
@@ -635,6 +668,7 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const Fu
     Params P;
     double T, a, b;
     prologue_range_wave(A, H, q, lane, P, T, a, b);
+    DH_STAMP_T(A, 28, 0);
     const int64_t p = (int64_t)((unsigned)q / (unsigned)H.tpp);
     const int g = (int)((unsigned)q % (unsigned)H.tpp);
     int2 gr = make_int2((int)p, 1);
@@ -661,6 +695,7 @@ __device__ __forceinline__ void table_prologue_wave(const PriceArgs& A, const Fu
     CC.half_sj2 = 0.5 * (P.sj * P.sj);
     CC.muj = P.muj;
     CC.lt = P.lam * T;
+    DH_STAMP_T(A, 30, 0);
     const int kcf =
         with_cut ? cf_cut_wave(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, lane) : 0;
     if (lane == 0) {
@@ -2203,6 +2238,7 @@ __global__ __launch_bounds__(kBlock, WV) void cos_fused_kernel(
     // scalar load's wait) and its value used after the staging barrier, so it overlaps the
     // prologue instead of delaying it (a halted launch wastes the prologue only)
     const int live_v = *(const __attribute__((address_space(1))) int*)H.live;
+    karg_prefetch_lines();
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ double shc[kTabC];
     __shared__ double red[4][1];

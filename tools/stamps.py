@@ -76,7 +76,8 @@ def main():
                   f"max {c.max():8.0f} cycles")
         life = st[:, 5] - st[:, 0]
         print(f"  lifetime median {np.median(life):8.0f}  max {life.max():8.0f}")
-        detail = [("prologue (thread 0)", 0, 8), ("staging wait", 8, 1),
+        detail = [("prologue (thread 0)", 0, 8), ("p: record+T in", 0, 31), ("p: range", 31, 28),
+                  ("p: exps+consts", 28, 30), ("p: to end", 30, 8), ("staging wait", 8, 1),
                   ("cf: consts load", 1, 6), ("cf: clamp scan", 1, 29), ("cf: after scan", 29, 6), ("cf: entries", 6, 7), ("cf: clamp+barrier", 7, 2),
                   ("cf: start w1 - w0", 6, 19), ("cf: start w3 - w0", 6, 20),
                   ("cf: end w1 - w0", 7, 16), ("cf: end w2 - w0", 7, 17),
