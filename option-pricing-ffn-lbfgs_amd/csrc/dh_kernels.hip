@@ -573,7 +573,8 @@ static_assert(sizeof(FusedKargsKP) + 256 <= 4096, "kernel arguments over 4 KiB")
 #ifndef DH_KARG_PREFETCH
 #define DH_KARG_PREFETCH 1
 #endif
-// The kernel-argument lines the fused kernel reads PriceArgs from (in place, karg_ref), pulled
+// The kernel-argument lines the fused kernel reads PriceArgs from (in place, karg_ref; the step
+// kernel's LbArgs lie in the same byte range), pulled
 // into the scalar cache in ONE round trip at entry: one s_load_dword per 64-byte line brings the
 // whole line, and the wave waits once.  Without it the prologue's path met each line as its own
 // dependent round trip (xcd_table's switch, the ahead stride, the tail-cut and table fields: five
@@ -4224,6 +4225,7 @@ __global__ __launch_bounds__(64) void lb_step_kernel(
     LbSlot* __restrict__ h_states, const double* __restrict__ h_part, int h_ntiles, int h_mode,
     int h_part_mode, int h_l0, int h_l1, int h_l2, int h_l3, LbArgs A_) {
     const LbArgs& A = karg_ref<LbArgs, kLbArgsKernargOff>();   // read in place (karg_ref)
+    karg_prefetch_lines();                             // LbArgs spans the same lines
     __shared__ double ring[kLbRing + dhlb::kM];
     __shared__ double fl[dhlb::kLanes];
     __shared__ double pb[dhlb::kLanes], pp[dhlb::kLanes];
