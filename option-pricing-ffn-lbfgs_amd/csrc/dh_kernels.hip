@@ -570,6 +570,9 @@ constexpr int kFusedParamsKernargOff = 384;
 static_assert(offsetof(FusedKargsKP, pb) == kFusedParamsKernargOff, "param block kernarg offset");
 static_assert(sizeof(FusedKargsKP) + 256 <= 4096, "kernel arguments over 4 KiB");
 
+#ifndef DH_PRE_GROUP8
+#define DH_PRE_GROUP8 1
+#endif
 #ifndef DH_KARG_PREFETCH
 #define DH_KARG_PREFETCH 1
 #endif
@@ -928,6 +931,71 @@ __global__ __launch_bounds__(kBlock) void table_prologue_kernel(PriceArgs A, int
     const int64_t q = gid / kPreLanes;
     const int sub = (int)(gid % kPreLanes);
     if (q >= n_q) return;                                      // whole groups (kBlock % 8 == 0)
+#if DH_PRE_GROUP8
+    // the chain spread over the group as in ahead_write: the two factors' cumulants on sub-lanes 0
+    // and 1, the six exponentials one per sub-lane, shuffled to the group -- table_prologue's
+    // expressions on the same operands, uncontracted, so the same bits
+  {
+#pragma clang fp contract(off)
+    const int tpp = tabs_per_p(A);
+    const int64_t p = A.p0 + q / tpp;
+    const int g = (int)(q % tpp);
+    const Params P = dh::load_params(A.prm + p * DH_PARAM_STRIDE);
+    const double T = A.paired ? A.T[p] : A.group_T[g];
+    int2 gr = make_int2((int)p, 1);
+    if (!A.paired) gr = A.groups[g];
+    const bool two = sub & 1;
+    const double v0 = two ? P.v02 : P.v01, k = two ? P.k2 : P.k1, th = two ? P.t2 : P.t1;
+    const double sg = two ? P.s2 : P.s1, rh = two ? P.r2 : P.r1;
+    double c1j, c2j;
+    dh::factor_cumulants(T, P.r, v0, k, th, sg, rh, c1j, c2j);   // double_heston.py:101-118
+    const double c1 = grp8_bcast(c1j, 0) + grp8_bcast(c1j, 1) + P.lam * T * P.muj;
+    const double c2 = grp8_bcast(c2j, 0) + grp8_bcast(c2j, 1) +
+                      P.lam * T * (P.sj * P.sj + P.muj * P.muj);
+    const double h = A.L * sqrt(fabs(c2));
+    const double a = c1 - h;                       // trunc_unclamped (double_heston.py:120-132)
+    const double b = c1 + h;
+    const int e_lane = sub < 6 ? sub : 0;
+    const double arg = e_lane == 0 ? b : e_lane == 1 ? a : e_lane == 2 ? a + 0.1
+                     : e_lane == 3 ? b - 0.1 : e_lane == 4 ? P.muj + 0.5 * (P.sj * P.sj)
+                     : -P.r * T;
+    const double e = exp(arg);
+    const double eb = grp8_bcast(e, 0), ea = grp8_bcast(e, 1), e2 = grp8_bcast(e, 2);
+    const double e3 = grp8_bcast(e, 3), e4 = grp8_bcast(e, 4), e5 = grp8_bcast(e, 5);
+    const int kcf = cf_cut_group8(P, T, a, b, tail_delta(A.tail, P.S0, b - a, A.N), A.N, sub);
+    if (sub == 0) {
+        const dh::FactorC F1 = dh::factor_consts(P.v01, P.k1, P.t1, P.s1, P.r1);
+        const dh::FactorC F2 = dh::factor_consts(P.v02, P.k2, P.t2, P.s2, P.r2);
+        const double comp = e4 - 1.0;              // cf_consts
+        double* o = out + q * kTabC;
+        o[0] = a;
+        o[1] = b;
+        o[2] = eb;
+        o[3] = ea;
+        o[4] = 2.0 / (b - a);
+        o[5] = dh::kPi / (b - a);
+        const double* f1 = (const double*)&F1;
+        const double* f2 = (const double*)&F2;
+        for (int i = 0; i < 6; ++i) {
+            o[6 + i] = f1[i];
+            o[12 + i] = f2[i];
+        }
+        o[18] = (P.r - P.q - P.lam * comp) * T;    // drift
+        o[19] = 0.5 * (P.sj * P.sj);               // half_sj2
+        o[20] = P.muj;
+        o[21] = P.lam * T;                         // lt
+        o[22] = P.S0;
+        o[23] = P.r;
+        o[24] = T;
+        o[25] = e2 * (1.0 + kClampMargin);
+        o[26] = e3 * (1.0 - kClampMargin);
+        o[27] = gr.x;
+        o[28] = gr.y;
+        o[29] = e5;
+        o[30] = kcf;
+    }
+  }
+#else
     double c[kTabC];
     table_prologue(A, q, c, false);
     const int tpp = tabs_per_p(A);
@@ -939,6 +1007,7 @@ __global__ __launch_bounds__(kBlock) void table_prologue_kernel(PriceArgs A, int
         double* o = out + q * kTabC;
         for (int i = 0; i < kTabC; ++i) o[i] = c[i];
     }
+#endif
 }
 
 #ifndef DH_TABLE_WAVES
