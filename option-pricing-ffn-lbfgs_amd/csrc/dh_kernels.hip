@@ -4185,6 +4185,10 @@ struct LbKargs {            // lb_step_kernel's argument list as a struct (its k
     LbArgs A;
 };
 static_assert(offsetof(LbKargs, A) == kLbArgsKernargOff, "LbArgs kernarg offset");
+// karg_prefetch_lines reads up to byte 0x1b4: inside the explicit arguments and the 256 bytes of
+// implicit ones every HIP kernel's segment carries after them
+static_assert(sizeof(LbKargs) + 256 >= 0x1b4, "kernel-argument prefetch past the segment");
+static_assert(sizeof(FusedKargs) + 256 >= 0x1b4, "kernel-argument prefetch past the segment");
 
 // live_inline[slot] as a scalar load straight from the kernel-argument segment; indexing the
 // by-value argument compiled to a flat load
