@@ -88,8 +88,14 @@ def main():
                   ("sums: finalise", 11, 4), ("loss: barrier", 4, 13), ("loss: wave sums", 13, 14),
                   ("loss: store drain", 14, 15), ("loss: ticket", 15, 12), ("loss: last", 12, 5)]
         for nm, i0, i1 in detail:
-            c = st[:, i1] - st[:, i0]
-            print(f"    {nm:20s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}")
+            # blocks that skip a phase (e.g. the prologue's "p:" stamps on blocks that load their
+            # constants formed ahead) leave its stamps at 0: only blocks with both stamps count
+            both = (st[:, i0] > 0) & (st[:, i1] > 0)
+            if not both.any():
+                continue
+            c = (st[both, i1] - st[both, i0]).astype(np.int64)
+            print(f"    {nm:20s} median {np.median(c):8.0f}  p90 {np.percentile(c, 90):8.0f}"
+                  + (f"  ({both.sum()} blocks)" if not both.all() else ""))
         if args.timeline:
             timeline(st[:, 23])
             hw = st[:, 24:28].astype(np.int64)
