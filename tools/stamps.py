@@ -156,7 +156,9 @@ def main():
 
 def timeline(rt):
     """Resident fused blocks over the launch from the 100 MHz start/end stamps (10 ns ticks)."""
-    t0 = (rt >> 32).astype(np.int64)
+    # the slot is read as int64: mask the shifted start, or a start stamp with bit 31 set comes back
+    # negative (and every residency as 2^32 ticks)
+    t0 = ((rt >> 32) & 0xffffffff).astype(np.int64)
     t1 = (rt & 0xffffffff).astype(np.int64)
     t1 = np.where(t1 < t0, t1 + (1 << 32), t1)
     base = t0.min()
